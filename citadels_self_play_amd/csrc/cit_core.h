@@ -1,0 +1,277 @@
+// Packed game state, rules tables and the CPython/numpy MT19937 restatement.
+//
+// One game = one fixed-width `CitGame` row (CIT_GAME_BYTES).  Rows live in HBM
+// as [B][CIT_GAME_BYTES] and are staged into LDS, one row per lane, by the
+// kernels in cit_hip.hip.  Everything here is plain C++ usable from host code
+// too (the test-only host build, cit_host.cpp); CIT_HD marks it for both.
+//
+// Reference correspondence (davpat108/CITADELS_self_play):
+//   CitPlayer            Agent state            game/agent.py:10-29
+//   CitGame              Game state             game/game.py:420-540
+//   gs_* / nx_*          GameState + next       game/helper_classes.py:16-34
+//   kh*                  HandKnowledge lists    game/helper_classes.py:37-43
+//   CitPlayer::kr        RoleKnowlage           game/helper_classes.py:45-70
+//   CitMT                CPython `random` / numpy RandomState (MT19937)
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define CIT_HD __host__ __device__ __forceinline__
+#define CIT_HDI __host__ __device__
+#else
+#define CIT_HD inline
+#define CIT_HDI inline
+#endif
+
+// ---------------------------------------------------------------- capacities
+#define CIT_NP 6
+#define CIT_HAND_CAP 32
+#define CIT_BUILD_CAP 16
+#define CIT_JD_CAP 24
+#define CIT_MUSEUM_CAP 16
+#define CIT_DECK_CAP 128          // ring buffer, power of two
+#define CIT_DISCARD_CAP 80
+#define CIT_USED_CAP 80
+#define CIT_KH_MAX 32
+#define CIT_KH_POOL 252
+#define CIT_SEVEN_CAP 8
+
+// ------------------------------------------------------------------- errors
+// A lane whose reference run would raise (or that overflows a fixed capacity)
+// stops with one of these bits set in CitGame::err.
+#define CIT_ERR_OVERFLOW 0x1u      // a fixed-capacity container overflowed
+#define CIT_ERR_EMPTY 0x2u         // random.choice([]) -> IndexError
+#define CIT_ERR_KEY 0x4u           // role_properties[-1] / role_to_role_id[None] -> KeyError
+#define CIT_ERR_VALUE 0x8u         // list.remove / list.index of a missing item -> ValueError
+#define CIT_ERR_INDEX 0x10u        // used_roles[i+1] past the end -> IndexError
+#define CIT_ERR_ATTR 0x20u         // get_player_from_role_id(..) is None -> AttributeError
+#define CIT_ERR_UNSUPPORTED 0x40u  // a branch this build does not implement
+#define CIT_ERR_NONE_OPTIONS 0x80u // get_options fell through and returned None
+
+// --------------------------------------------------------------- card codes
+// code < 40: type_ID with its table suit; 40..44: Magic School (type 25)
+// re-suited to suit code-40 (option_functions.py:147-153).
+enum { SUIT_TRADE = 0, SUIT_WAR, SUIT_RELIGION, SUIT_LORD, SUIT_UNIQUE };
+#define CIT_NO_CARD 255
+
+CIT_HD int card_type(int c) { return c >= 40 ? 25 : c; }
+CIT_HD int type_suit(int t) { return t < 6 ? 0 : t < 10 ? 1 : t < 13 ? 2 : t < 16 ? 3 : 4; }
+CIT_HD int card_suit(int c) { return c >= 40 ? c - 40 : type_suit(c); }
+// config.py costs, 3 bits per type (types 0..19 / 20..39).
+#define CIT_COST_LO 0x059dae168d69d511ull
+#define CIT_COST_HI 0x0ba5d2eb5e7b5d6eull
+CIT_HD int type_cost(int t) {
+  return t < 20 ? (int)((CIT_COST_LO >> (3 * t)) & 7) : (int)((CIT_COST_HI >> (3 * (t - 20))) & 7);
+}
+CIT_HD int card_cost(int c) { return type_cost(card_type(c)); }
+
+// -------------------------------------------------------------------- roles
+// role index = rank*3 + variant (config.py:82-91); 27 = "Bewitched", 255 = None.
+#define ROLE_BEWITCHED 27
+#define ROLE_NONE 255
+enum {
+  R_ASSASSIN = 0, R_WITCH, R_MAGISTRATE, R_THIEF, R_SPY, R_BLACKMAILER, R_MAGICIAN, R_WIZARD,
+  R_SEER, R_KING, R_EMPEROR, R_PATRICIAN, R_BISHOP, R_ABBOT, R_CARDINAL, R_MERCHANT, R_ALCHEMIST,
+  R_TRADER, R_ARCHITECT, R_NAVIGATOR, R_SCHOLAR, R_WARLORD, R_DIPLOMAT, R_MARSHAL, R_QUEEN,
+  R_ARTIST, R_TAXCOLLECTOR
+};
+
+// ------------------------------------------------------------ option names
+// ids follow option.py:34-45 (generate_name_to_id_map)
+enum {
+  O_ROLE_PICK = 0, O_GOLD_OR_CARD, O_WHICH_CARD, O_BLACKMAIL_RESPONSE, O_REVEAL_BLACKMAIL,
+  O_REVEAL_WARRANT, O_BUILD, O_EMPTY, O_FINISH_ROUND, O_GHOST_TOWN, O_SMITHY, O_LAB,
+  O_MAGIC_SCHOOL, O_WEAPON_STORAGE, O_LIGHTHOUSE, O_MUSEUM, O_GRAVEYARD, O_TAKE_GOLD_WAR,
+  O_ASSASSINATION, O_MAGISTRATE_WARRANT, O_BEWITCHING, O_STEAL, O_BLACKMAIL, O_SPY,
+  O_MAGIC_HAND_CHANGE, O_DISCARD_AND_DRAW, O_LOOK_AT_HAND, O_TAKE_FROM_HAND, O_SEER,
+  O_GIVE_BACK_CARD, O_TAKE_CROWN_KING, O_GIVE_CROWN, O_TAKE_CROWN_PAT, O_BISHOP, O_CARDINAL,
+  O_ABBOT_GOLD_OR_CARD, O_ABBOT_BEG, O_MERCHANT, O_ALCHEMIST, O_TRADER, O_ARCHITECT,
+  O_NAVIGATOR, O_SCHOLAR, O_SCHOLAR_PICK, O_WARLORD, O_MARSHAL, O_DIPLOMAT, O_NUM_NAMES
+};
+
+// already_done_moves tokens, counted (only `in` / `.count` are ever asked of the list)
+enum { ADM_BEGGED = 0, ADM_ABILITY, ADM_LAB, ADM_MAGIC_SCHOOL, ADM_MUSEUM, ADM_NON_TRADE, ADM_SMITHY,
+       ADM_TAKE_GOLD, ADM_TRADE, ADM_N };
+
+// ------------------------------------------------------------- option desc
+// 16-byte option descriptor; field meaning per name is documented in
+// include/citadels.h (CitOption).
+struct CitOpt {
+  uint8_t name, perp;
+  int8_t target;
+  uint8_t a, b, c, d, flags;
+  uint64_t x;
+};
+
+// ------------------------------------------------------------- packed game
+struct CitPlayer {                 // 112 B
+  uint8_t hand[CIT_HAND_CAP];
+  uint8_t build[CIT_BUILD_CAP];
+  uint8_t jd[CIT_JD_CAP];          // just_drawn_cards
+  uint8_t museum[CIT_MUSEUM_CAP];
+  uint8_t n_hand, n_build, n_jd, n_museum;
+  int16_t gold;
+  uint8_t role;                    // role index / ROLE_BEWITCHED / ROLE_NONE
+  int8_t replicas;                 // False/True/int semantics of agent.replicas
+  uint8_t flags;                   // PF_*
+  uint8_t pad0;
+  uint16_t kr[CIT_NP];             // RoleKnowlage: bits 0..8 = ids -1..7, bit 15 confirmed
+  uint16_t pad1;
+};
+enum { PF_CROWN = 1, PF_LIGHTHOUSE = 2, PF_FIRST7 = 4, PF_WITCH = 8 };
+#define KR_CONFIRMED 0x8000u
+
+struct CitKH {                     // one HandKnowledge entry, 4 B
+  uint8_t owner;                   // whose known_hands list
+  int8_t target;                   // player_id (-1 = deck)
+  uint8_t conf_flags;              // conf (bits 0..3) | wizard 0x10 | used 0x20
+  uint8_t len;                     // cards are kh_pool[off..off+len), off = running sum
+};
+
+struct CitGame {
+  CitPlayer pl[CIT_NP];            // 672
+  uint8_t deck[CIT_DECK_CAP];      // ring: logical i at (deck_head+i) & (CAP-1)
+  uint8_t discard[CIT_DISCARD_CAP];
+  uint8_t used_cards[CIT_USED_CAP];
+  uint8_t kh_pool[CIT_KH_POOL];
+  CitKH kh[CIT_KH_MAX];            // ordered as appended; per-owner order = list order
+  uint8_t deck_head, n_deck, n_discard, n_used_cards;
+  uint8_t n_kh, kh_fill, preset, pad2;
+  uint8_t roles[8];                // role index per rank
+  uint8_t rtc;                     // roles_to_choose_from: rank bitmask (ascending)
+  uint8_t n_used_roles;            // 255 = attribute absent
+  int8_t used_roles[CIT_NP];       // sorted role ids
+  uint8_t turn[CIT_NP];            // turn_orders_for_roles
+  uint8_t rp[8];                   // RolePropery: RP_* bits
+  // current GameState
+  uint8_t gs_state;
+  int8_t gs_pid;                   // -1 = None (before the first setup_round)
+  uint8_t gs_adm[ADM_N];
+  uint8_t gs_intr;
+  // next_gamestate (always a fresh GameState(state=5,...) in the reference)
+  uint8_t nx_valid, nx_state;
+  int8_t nx_pid;
+  uint8_t nx_adm[ADM_N];
+  uint8_t nx_intr, nx_alias, nx_hasnext;
+  uint8_t ending, terminal;
+  int8_t winner;
+  uint8_t has_points;
+  int16_t points[CIT_NP];
+  uint8_t warrant;                 // warrant_building card, CIT_NO_CARD = absent
+  uint8_t n_seer;                  // 255 = seer_taken_card_from absent
+  uint8_t seer_from[5];
+  uint8_t seven_kind;              // 0 absent, 1 Deck, 2 plain [] (after put-back)
+  uint8_t n_seven;
+  uint8_t seven[CIT_SEVEN_CAP];
+  uint8_t n_sch;                   // scholar picks prepared by get_options (state 9)
+  uint8_t sch[CIT_SEVEN_CAP];
+  uint32_t err;
+  uint32_t steps;                  // carry_out calls applied to this game
+};
+enum { RP_DEAD = 1, RP_WARRANT_SHIFT = 1, RP_POSSESSED = 8, RP_ROBBED = 16, RP_BLACKMAIL_SHIFT = 5 };
+enum { WB_NONE = 0, WB_REAL = 1, WB_FAKE = 2 };
+
+#define CIT_GAME_BYTES 1456
+static_assert(sizeof(CitGame) <= CIT_GAME_BYTES, "CitGame grew past its row size");
+static_assert(CIT_GAME_BYTES % 16 == 0, "row must be 16-byte aligned");
+
+// ----------------------------------------------------------------- MT19937
+// Per-lane MT19937 laid out structure-of-arrays: word i of lane l at
+// mt[i*stride + l]; idx[l] is the position (624 = twist next).
+#define CIT_MT_N 624
+struct CitMT {
+  uint32_t* mt;
+  uint32_t* idx;
+  int stride;
+};
+
+CIT_HD uint32_t mt_word(const CitMT& r, int i) { return r.mt[(long)i * r.stride]; }
+CIT_HD void mt_set(const CitMT& r, int i, uint32_t v) { r.mt[(long)i * r.stride] = v; }
+
+// init_genrand (numpy legacy `RandomState.seed(int)`)
+CIT_HDI void mt_init_genrand(const CitMT& r, uint32_t s) {
+  mt_set(r, 0, s);
+  for (int i = 1; i < CIT_MT_N; i++) {
+    s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i;
+    mt_set(r, i, s);
+  }
+  *r.idx = CIT_MT_N;
+}
+
+// CPython random.seed(int): init_by_array(key = 32-bit little-endian words of |seed|)
+CIT_HDI void mt_seed_cpython(const CitMT& r, uint64_t seed) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  int klen = (seed >> 32) ? 2 : 1;
+  mt_init_genrand(r, 19650218u);
+  int i = 1, j = 0;
+  uint32_t prev = mt_word(r, 0);
+  for (int k = (CIT_MT_N > klen ? CIT_MT_N : klen); k; k--) {
+    uint32_t v = (mt_word(r, i) ^ ((prev ^ (prev >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+    mt_set(r, i, v);
+    prev = v;
+    i++;
+    j++;
+    if (i >= CIT_MT_N) { mt_set(r, 0, v); i = 1; }
+    if (j >= klen) j = 0;
+  }
+  for (int k = CIT_MT_N - 1; k; k--) {
+    uint32_t v = (mt_word(r, i) ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
+    mt_set(r, i, v);
+    prev = v;
+    i++;
+    if (i >= CIT_MT_N) { mt_set(r, 0, v); i = 1; }
+  }
+  mt_set(r, 0, 0x80000000u);
+  *r.idx = CIT_MT_N;
+}
+
+CIT_HDI void mt_twist(const CitMT& r) {
+  uint32_t cur = mt_word(r, 0);
+  for (int i = 0; i < CIT_MT_N; i++) {
+    // the last word pairs with the already-rewritten mt[0], as in genrand's tail step
+    uint32_t nxt = (i + 1 < CIT_MT_N) ? mt_word(r, i + 1) : mt_word(r, 0);
+    uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+    int m = i + 397;
+    uint32_t far = m < CIT_MT_N ? mt_word(r, m) : mt_word(r, m - CIT_MT_N);
+    uint32_t v = far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    mt_set(r, i, v);
+    cur = nxt;
+  }
+}
+
+CIT_HD uint32_t mt_next(const CitMT& r) {
+  uint32_t i = *r.idx;
+  if (i >= CIT_MT_N) {
+    mt_twist(r);
+    i = 0;
+  }
+  uint32_t y = mt_word(r, (int)i);
+  *r.idx = i + 1;
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+CIT_HD int bit_length(uint32_t n) {
+  int k = 0;
+  while (n) { k++; n >>= 1; }
+  return k;
+}
+
+// random._randbelow_with_getrandbits (Lib/random.py:239-249)
+CIT_HD uint32_t mt_randbelow(const CitMT& r, uint32_t n) {
+  if (!n) return 0;
+  int k = bit_length(n);
+  uint32_t v = mt_next(r) >> (32 - k);
+  while (v >= n) v = mt_next(r) >> (32 - k);
+  return v;
+}
+
+// random.random() / numpy random_sample(): 53-bit double from two draws
+CIT_HD double mt_random(const CitMT& r) {
+  uint32_t a = mt_next(r) >> 5, b = mt_next(r) >> 6;
+  return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
+}

@@ -1,0 +1,1454 @@
+// The rules engine on one packed game row: get_options (as an enumeration
+// into a sink, so a caller can count, pick the k-th, or materialise without a
+// per-lane option buffer) and carry_out.  Host+device (CIT_HD).
+//
+//   cit_get_options  = cit_prepare_options (mutating part) + cit_enum_options
+//                      game/agent.py:50-83, game/agent_functions.py:13-509
+//   cit_carry_out    = game/option.py:118-122 -> game/option_functions.py:6-631
+//   cit_setup_round  = game/game.py:144-171
+//   cit_init_game    = game/game.py:17-24,420-540 (+ run_utils.create_game)
+#pragma once
+#include "cit_core.h"
+
+// =========================================================== list helpers
+CIT_HD bool has_type(const uint8_t* a, int n, int t) {
+  for (int i = 0; i < n; i++)
+    if (card_type(a[i]) == t) return true;
+  return false;
+}
+CIT_HD int count_type(const uint8_t* a, int n, int t) {
+  int k = 0;
+  for (int i = 0; i < n; i++) k += card_type(a[i]) == t;
+  return k;
+}
+CIT_HD int count_suit(const uint8_t* a, int n, int s) {
+  int k = 0;
+  for (int i = 0; i < n; i++) k += card_suit(a[i]) == s;
+  return k;
+}
+// Deck.get_a_card_like_it (deck.py:49-55): removes the first card of c's type;
+// returns it, or c itself when there is none.
+CIT_HD int take_like(uint8_t* a, uint8_t& n, int c) {
+  int t = card_type(c);
+  for (int i = 0; i < n; i++) {
+    if (card_type(a[i]) == t) {
+      int r = a[i];
+      for (int j = i + 1; j < n; j++) a[j - 1] = a[j];
+      n--;
+      return r;
+    }
+  }
+  return c;
+}
+// Deck.add_card (deck.py:62-67): the "Deck Empty" sentinel (CIT_NO_CARD) is dropped.
+CIT_HD void put_card(CitGame& g, uint8_t* a, uint8_t& n, int cap, int c) {
+  if (c == CIT_NO_CARD) return;
+  if (n >= cap) { g.err |= CIT_ERR_OVERFLOW; return; }
+  a[n++] = (uint8_t)c;
+}
+CIT_HD int pop_front(uint8_t* a, uint8_t& n) {
+  if (!n) return CIT_NO_CARD;
+  int r = a[0];
+  for (int j = 1; j < n; j++) a[j - 1] = a[j];
+  n--;
+  return r;
+}
+
+#define HAND(p) (p).hand, (p).n_hand, CIT_HAND_CAP
+#define BUILD(p) (p).build, (p).n_build, CIT_BUILD_CAP
+#define JD(p) (p).jd, (p).n_jd, CIT_JD_CAP
+#define MUSEUM(p) (p).museum, (p).n_museum, CIT_MUSEUM_CAP
+CIT_HD bool p_has(const CitPlayer& p, int t) { return has_type(p.build, p.n_build, t); }
+
+// ------------------------------------------------------------ deck (ring)
+CIT_HD int deck_at(const CitGame& g, int i) { return g.deck[(g.deck_head + i) & (CIT_DECK_CAP - 1)]; }
+CIT_HD uint8_t& deck_ref(CitGame& g, int i) { return g.deck[(g.deck_head + i) & (CIT_DECK_CAP - 1)]; }
+CIT_HD int deck_draw(CitGame& g) {
+  if (!g.n_deck) return CIT_NO_CARD;
+  int c = g.deck[g.deck_head];
+  g.deck_head = (uint8_t)((g.deck_head + 1) & (CIT_DECK_CAP - 1));
+  g.n_deck--;
+  return c;
+}
+CIT_HD void deck_put(CitGame& g, int c) {
+  if (c == CIT_NO_CARD) return;
+  if (g.n_deck >= CIT_DECK_CAP - 1) { g.err |= CIT_ERR_OVERFLOW; return; }
+  deck_ref(g, g.n_deck) = (uint8_t)c;
+  g.n_deck++;
+}
+CIT_HD int deck_take_like(CitGame& g, int c) {
+  int t = card_type(c);
+  for (int i = 0; i < g.n_deck; i++) {
+    if (card_type(deck_at(g, i)) == t) {
+      int r = deck_at(g, i);
+      for (int j = i + 1; j < g.n_deck; j++) deck_ref(g, j - 1) = (uint8_t)deck_at(g, j);
+      g.n_deck--;
+      return r;
+    }
+  }
+  return c;
+}
+// random.shuffle (Lib/random.py:380-392) over any indexable sequence
+template <class At>
+CIT_HD void shuffle_seq(const CitMT& rng, int n, At at) {
+  for (int i = n - 1; i > 0; i--) {
+    int j = (int)mt_randbelow(rng, (uint32_t)(i + 1));
+    uint8_t t = at(i);
+    at(i) = at(j);
+    at(j) = t;
+  }
+}
+CIT_HD void shuffle_arr(const CitMT& rng, uint8_t* a, int n) {
+  shuffle_seq(rng, n, [a](int i) -> uint8_t& { return a[i]; });
+}
+CIT_HD void deck_shuffle(CitGame& g, const CitMT& rng) {
+  shuffle_seq(rng, g.n_deck, [&g](int i) -> uint8_t& { return deck_ref(g, i); });
+}
+// reshuffle_deck_if_empty (option_functions.py:564-570)
+CIT_HD void reshuffle_if_empty(CitGame& g, const CitMT& rng) {
+  if (g.n_deck || !g.n_discard) return;
+  shuffle_arr(rng, g.discard, g.n_discard);
+  g.deck_head = 0;
+  for (int i = 0; i < g.n_discard; i++) g.deck[i] = g.discard[i];
+  g.n_deck = g.n_discard;
+  g.n_discard = 0;
+}
+CIT_HD void draw_into(CitGame& g, const CitMT& rng, uint8_t* a, uint8_t& n, int cap, int k) {
+  for (int i = 0; i < k; i++) {
+    reshuffle_if_empty(g, rng);
+    put_card(g, a, n, cap, deck_draw(g));
+  }
+}
+
+// ------------------------------------------------------ hand knowledge pool
+CIT_HD int kh_conf(const CitKH& e) { return e.conf_flags & 15; }
+CIT_HD int kh_off(const CitGame& g, int e) {
+  int o = 0;
+  for (int i = 0; i < e; i++) o += g.kh[i].len;
+  return o;
+}
+template <class At>
+CIT_HD void kh_append(CitGame& g, int owner, int target, int conf, bool wizard, int n, At card_at) {
+  if (g.n_kh >= CIT_KH_MAX || g.kh_fill + n > CIT_KH_POOL) { g.err |= CIT_ERR_OVERFLOW; return; }
+  CitKH& e = g.kh[g.n_kh++];
+  e.owner = (uint8_t)owner;
+  e.target = (int8_t)target;
+  e.conf_flags = (uint8_t)(conf | (wizard ? 0x10 : 0));
+  e.len = (uint8_t)n;
+  for (int i = 0; i < n; i++) g.kh_pool[g.kh_fill + i] = (uint8_t)card_at(i);
+  g.kh_fill = (uint8_t)(g.kh_fill + n);
+}
+// get_a_card_like_it on one entry's hand
+CIT_HD void kh_take_like(CitGame& g, int e, int c) {
+  int off = kh_off(g, e), n = g.kh[e].len, t = card_type(c);
+  for (int i = 0; i < n; i++) {
+    if (card_type(g.kh_pool[off + i]) == t) {
+      for (int j = off + i + 1; j < g.kh_fill; j++) g.kh_pool[j - 1] = g.kh_pool[j];
+      g.kh[e].len--;
+      g.kh_fill--;
+      return;
+    }
+  }
+}
+// substract_from_known_hand_confidences_and_clear_wizard (agent.py:100-109), all owners
+CIT_HD void kh_decay(CitGame& g) {
+  int w = 0, wo = 0, ro = 0;
+  for (int e = 0; e < g.n_kh; e++) {
+    CitKH k = g.kh[e];
+    int conf = kh_conf(k) - 1;
+    int len = k.len;
+    if (conf != 0) {
+      for (int i = 0; i < len; i++) g.kh_pool[wo + i] = g.kh_pool[ro + i];
+      k.conf_flags = (uint8_t)(conf & 15);
+      g.kh[w++] = k;
+      wo += len;
+    }
+    ro += len;
+  }
+  g.n_kh = (uint8_t)w;
+  g.kh_fill = (uint8_t)wo;
+}
+
+// ------------------------------------------------------------------ roles
+// role_to_role_id (config.py:93-121); ROLE_NONE is a KeyError
+CIT_HD int role_rank(CitGame& g, int role) {
+  if (role == ROLE_BEWITCHED) return -1;
+  if (role >= 27) { g.err |= CIT_ERR_KEY; return 0; }
+  return role / 3;
+}
+// role_properties[role_to_role_id[role]]: the dict has keys 0..7 only
+CIT_HD uint8_t& rp_of(CitGame& g, int role) {
+  int r = role_rank(g, role);
+  if (r < 0) { g.err |= CIT_ERR_KEY; r = 0; }
+  return g.rp[r];
+}
+CIT_HD int rp_warrant(uint8_t v) { return (v >> RP_WARRANT_SHIFT) & 3; }
+CIT_HD int rp_blackmail(uint8_t v) { return (v >> RP_BLACKMAIL_SHIFT) & 3; }
+CIT_HD int role_of_id(const CitGame& g, int rid) { return rid < 0 ? ROLE_BEWITCHED : g.roles[rid]; }
+// get_player_from_role_id (game.py:403-412); -1 for None
+CIT_HD int holder(const CitGame& g, int rid) {
+  int want = role_of_id(g, rid);
+  for (int i = 0; i < CIT_NP; i++)
+    if (g.pl[i].role == want) return i;
+  return -1;
+}
+CIT_HD int holder_checked(CitGame& g, int rid) {
+  int h = holder(g, rid);
+  if (h < 0) { g.err |= CIT_ERR_ATTR; return 0; }
+  return h;
+}
+
+// ---------------------------------------------------------- game states
+CIT_HD void gs_set(CitGame& g, int state, int pid) {
+  g.gs_state = (uint8_t)state;
+  g.gs_pid = (int8_t)pid;
+}
+CIT_HD void gs_append(CitGame& g, int tok) {
+  g.gs_adm[tok]++;
+  if (g.nx_valid && g.nx_alias) g.nx_adm[tok]++;
+}
+// next_gamestate = GameState(state=5, player_id=pid, already_done_moves=<alias|fresh|[ability]>)
+enum { NX_FRESH = 0, NX_ALIAS = 1, NX_ABILITY = 2 };
+CIT_HD void gs_make_next(CitGame& g, int pid, int mode) {
+  g.nx_valid = 1;
+  g.nx_state = 5;
+  g.nx_pid = (int8_t)pid;
+  for (int i = 0; i < ADM_N; i++) g.nx_adm[i] = mode == NX_ALIAS ? g.gs_adm[i] : 0;
+  if (mode == NX_ABILITY) g.nx_adm[ADM_ABILITY] = 1;
+  g.nx_intr = 0;
+  g.nx_alias = mode == NX_ALIAS;
+  g.nx_hasnext = 0;
+}
+// game.gamestate = game.gamestate.next_gamestate
+CIT_HD void gs_goto_next(CitGame& g) {
+  if (!g.nx_valid) { g.err |= CIT_ERR_ATTR; return; }
+  g.gs_state = g.nx_state;
+  g.gs_pid = g.nx_pid;
+  for (int i = 0; i < ADM_N; i++) g.gs_adm[i] = g.nx_adm[i];
+  g.gs_intr = g.nx_intr;
+  g.nx_valid = 0;
+  g.nx_alias = 0;
+}
+// a brand-new GameState(state, pid) replaces the current one
+CIT_HD void gs_fresh(CitGame& g, int state, int pid) {
+  gs_set(g, state, pid);
+  for (int i = 0; i < ADM_N; i++) g.gs_adm[i] = 0;
+  g.gs_intr = 0;
+  g.nx_valid = 0;
+  g.nx_alias = 0;
+}
+CIT_HD void gs_rebind_adm(CitGame& g) {   // gamestate.already_done_moves = []
+  for (int i = 0; i < ADM_N; i++) g.gs_adm[i] = 0;
+  g.nx_alias = 0;
+}
+CIT_HD void at5(CitGame& g, int pid, int tok) {
+  gs_set(g, 5, pid);
+  if (tok >= 0) gs_append(g, tok);
+}
+
+// ================================================================= setup
+// refresh_used_roles (game.py:349-357)
+CIT_HD void refresh_used_roles(CitGame& g) {
+  int8_t v[CIT_NP];
+  for (int i = 0; i < CIT_NP; i++) v[i] = (int8_t)role_rank(g, g.pl[i].role);
+  for (int i = 1; i < CIT_NP; i++) {     // insertion sort
+    int8_t x = v[i];
+    int j = i - 1;
+    while (j >= 0 && v[j] > x) { v[j + 1] = v[j]; j--; }
+    v[j + 1] = x;
+  }
+  for (int i = 0; i < CIT_NP; i++) g.used_roles[i] = v[i];
+  g.n_used_roles = CIT_NP;
+}
+// setup_next_player (game.py:391-401); current < 0 means "no current player"
+CIT_HD void setup_next_player(CitGame& g, int current) {
+  if (g.gs_state == 0) {
+    refresh_used_roles(g);
+    g.gs_state = 1;
+    g.gs_pid = (int8_t)holder_checked(g, g.used_roles[0]);
+  } else if (current >= 0) {
+    g.gs_state = 1;
+    int r = role_rank(g, g.pl[current].role);
+    int i = -1;
+    for (int k = 0; k < g.n_used_roles; k++)
+      if (g.used_roles[k] == r) { i = k; break; }
+    if (i < 0) { g.err |= CIT_ERR_VALUE; return; }
+    if (i + 1 >= g.n_used_roles) { g.err |= CIT_ERR_INDEX; return; }
+    g.gs_pid = (int8_t)holder_checked(g, g.used_roles[i + 1]);
+    gs_rebind_adm(g);
+  } else {
+    g.err |= CIT_ERR_UNSUPPORTED;
+  }
+}
+
+CIT_HD void cit_setup_round(CitGame& g, const CitMT& rng) {
+  for (int r = 0; r < 8; r++) g.rp[r] = 0;
+  g.n_used_roles = 0;
+  uint8_t pool[8];
+  for (int r = 0; r < 8; r++) pool[r] = (uint8_t)r;
+  shuffle_arr(rng, pool, 8);
+  uint8_t m = 0;
+  for (int r = 0; r < 7; r++) m |= (uint8_t)(1u << pool[r]);   // pool[7] is the face-down role
+  g.rtc = m;
+  int c = -1;
+  for (int i = 0; i < CIT_NP; i++)
+    if (g.pl[i].flags & PF_CROWN) { c = i; break; }
+  if (c < 0) { g.err |= CIT_ERR_UNSUPPORTED; return; }     // turn order would double (game.py:164-165)
+  uint8_t t[CIT_NP];
+  for (int i = 0; i < CIT_NP; i++) t[i] = g.turn[(i + c) % CIT_NP];
+  for (int i = 0; i < CIT_NP; i++) g.turn[i] = t[i];
+  gs_fresh(g, 0, g.turn[0]);
+  kh_decay(g);
+  for (int i = 0; i < CIT_NP; i++)
+    for (int j = 0; j < CIT_NP; j++) g.pl[i].kr[j] = 0;
+}
+
+// Game(preset) + set_initial_variables + create_game's setup_round, for a
+// game whose CPython stream has just been seeded.
+CIT_HD void cit_init_game(CitGame& g, const CitMT& rng, bool preset) {
+  uint8_t* z = (uint8_t*)&g;
+  for (int i = 0; i < (int)sizeof(CitGame); i++) z[i] = 0;
+  // building_cards multiplicities per type 0..15, one nibble each (config.py:2-52)
+  const uint64_t kBaseCounts = 0x3543333233324335ull;
+  uint8_t uniq[24];
+  for (int i = 0; i < 24; i++) uniq[i] = (uint8_t)(i == 0 ? 16 : i == 1 || i == 2 ? 17 : i < 23 ? i + 15 : 39);
+  int n = 0;
+  for (int k = 0; k < 16; k++)
+    for (int j = 0; j < (int)((kBaseCounts >> (4 * k)) & 15); j++) g.deck[n++] = (uint8_t)k;
+  if (preset) {
+    for (int i = 0; i < 24; i++) g.deck[n++] = uniq[i];
+  } else {
+    // random.sample(unique_building_cards, 14): pool variant (Lib/random.py:483-490)
+    uint8_t pool[24];
+    for (int i = 0; i < 24; i++) pool[i] = uniq[i];
+    for (int i = 0; i < 14; i++) {
+      int j = (int)mt_randbelow(rng, (uint32_t)(24 - i));
+      g.deck[n++] = pool[j];
+      pool[j] = pool[24 - i - 1];
+    }
+  }
+  g.deck_head = 0;
+  g.n_deck = (uint8_t)n;
+  deck_shuffle(g, rng);
+  for (int i = 0; i < n; i++) g.used_cards[i] = g.deck[i];
+  g.n_used_cards = (uint8_t)n;
+  for (int i = 0; i < CIT_NP; i++) {
+    g.pl[i].gold = 2;
+    g.pl[i].role = ROLE_NONE;
+  }
+  if (preset) {
+    // set_preset hands (game.py:428-474), one byte per card
+    const uint64_t kHands[6] = {0x131211100000ull, 0x171615140101ull, 0x1b1a19180302ull,
+                                0x1f1e1d1c0403ull, 0x232221200004ull, 0x002725240100ull};
+    for (int p = 0; p < CIT_NP; p++)
+      for (int k = 0; k < 6; k++) put_card(g, HAND(g.pl[p]), deck_take_like(g, (int)((kHands[p] >> (8 * k)) & 0xFF)));
+    g.pl[3].flags |= PF_CROWN;
+    // Witch, Spy, Wizard, King, Abbot, Alchemist, Navigator, Warlord (game.py:479-486)
+    const uint64_t kRoles = 0x1513100d09070401ull;
+    for (int r = 0; r < 8; r++) g.roles[r] = (uint8_t)((kRoles >> (8 * r)) & 0xFF);
+    for (int i = 0; i < CIT_NP; i++) g.turn[i] = (uint8_t)i;
+  } else {
+    for (int k = 0; k < 4; k++)
+      for (int p = 0; p < CIT_NP; p++) put_card(g, HAND(g.pl[p]), deck_draw(g));
+    for (int r = 0; r < 8; r++) g.roles[r] = (uint8_t)(r * 3 + (int)mt_randbelow(rng, 3));
+    for (int i = 0; i < CIT_NP; i++) g.turn[i] = (uint8_t)i;
+    shuffle_arr(rng, g.turn, CIT_NP);
+    int crown = (int)mt_randbelow(rng, 6);
+    g.pl[crown].flags |= PF_CROWN;
+  }
+  g.preset = preset;
+  g.gs_pid = -1;
+  g.winner = -1;
+  g.warrant = CIT_NO_CARD;
+  g.n_seer = 255;
+  g.n_used_roles = 255;
+  cit_setup_round(g, rng);
+}
+
+// ============================================================ scoring
+CIT_HD int count_points(const CitPlayer& p) {           // agent.py:116-143
+  int pts = 0;
+  bool well = p_has(p, 31);
+  for (int i = 0; i < p.n_build; i++) {
+    int c = p.build[i], t = card_type(c);
+    pts += card_cost(c);
+    if (t == 18 || t == 23) pts += 2;
+    if (well && card_suit(c) == SUIT_UNIQUE) pts += 1;
+  }
+  if (p.n_build >= 7) pts += 2;
+  if (p.flags & PF_FIRST7) pts += 4;
+  pts += p.n_museum;
+  if (p_has(p, 37)) pts += p.gold;
+  if (p_has(p, 39)) pts += p.n_hand;
+  return pts;
+}
+// check_game_ending (game.py:359-368): winner index or -1
+CIT_HD int check_game_ending(CitGame& g) {
+  if (!g.ending) return -1;
+  int best = 0;
+  for (int i = 0; i < CIT_NP; i++) {
+    g.points[i] = (int16_t)count_points(g.pl[i]);
+    if (g.points[i] > g.points[best]) best = i;
+  }
+  g.has_points = 1;
+  g.terminal = 1;
+  g.winner = (int8_t)best;
+  return best;
+}
+// is_last_round (game.py:173-181)
+CIT_HD void is_last_round(CitGame& g) {
+  if (g.ending) return;
+  for (int i = 0; i < CIT_NP; i++)
+    if (g.pl[i].n_build == 7) {
+      g.ending = 1;
+      g.pl[i].flags |= PF_FIRST7;
+    }
+}
+
+// ======================================================= option helpers
+CIT_HD CitOpt mk(int name, int perp, int target = -1, int a = 0, int b = 0, int c = 0, int flags = 0,
+                 uint64_t x = 0) {
+  CitOpt o;
+  o.name = (uint8_t)name;
+  o.perp = (uint8_t)perp;
+  o.target = (int8_t)target;
+  o.a = (uint8_t)a;
+  o.b = (uint8_t)b;
+  o.c = (uint8_t)c;
+  o.d = 0;
+  o.flags = (uint8_t)flags;
+  o.x = x;
+  return o;
+}
+enum { OF_TUPLE = 1, OF_NEXT_WITCH = 1, OF_CROWN = 2, OF_BUILD = 1, OF_FACTORY = 1 };
+
+// Sinks: emit() returns true to stop the enumeration.
+struct CountSink {
+  int n = 0;
+  uint32_t err = 0;
+  CIT_HD bool emit(const CitOpt&) { n++; return false; }
+  template <class F> CIT_HD bool block(int cnt, F&&) { n += cnt; return false; }
+};
+struct PickSink {
+  int k;
+  CitOpt out;
+  uint32_t err = 0;
+  CIT_HD explicit PickSink(int kk) : k(kk) { out = mk(O_NUM_NAMES, 0); }
+  CIT_HD bool emit(const CitOpt& o) {
+    if (k == 0) { out = o; return true; }
+    k--;
+    return false;
+  }
+  template <class F> CIT_HD bool block(int cnt, F&& f) {
+    if (k < cnt) { out = f(k); return true; }
+    k -= cnt;
+    return false;
+  }
+};
+struct ListSink {
+  CitOpt* buf;
+  int cap;
+  int n = 0;
+  uint32_t err = 0;
+  CIT_HD ListSink(CitOpt* b, int c) : buf(b), cap(c) {}
+  CIT_HD bool emit(const CitOpt& o) {
+    if (n < cap) buf[n] = o;
+    n++;
+    return false;
+  }
+  template <class F> CIT_HD bool block(int cnt, F&& f) {
+    for (int i = 0; i < cnt; i++) {
+      if (n < cap) buf[n] = f(i);
+      n++;
+    }
+    return false;
+  }
+};
+
+#define EMIT(...)                                  \
+  do {                                             \
+    if (s.emit(__VA_ARGS__)) return true;          \
+  } while (0)
+
+// Python round(x/1e2) (half to even) on an integer count, floored at 1
+// (agent_functions.py:293,416).
+CIT_HD long subsample_stride(long c) {
+  long q = c / 100, r = c % 100;
+  if (r > 50 || (r == 50 && (q & 1))) q++;
+  return q < 1 ? 1 : q;
+}
+CIT_HD long binom(int n, int k) {
+  if (k < 0 || k > n) return 0;
+  if (k > n - k) k = n - k;
+  long r = 1;
+  for (int i = 1; i <= k; i++) r = r * (n - k + i) / i;
+  return r;
+}
+// lexicographic combination number `idx` of k items out of n (itertools.combinations order)
+CIT_HD uint64_t unrank_comb(int n, int k, long idx) {
+  uint64_t m = 0;
+  int x = 0;
+  for (int i = 0; i < k; i++) {
+    while (true) {
+      long c = binom(n - x - 1, k - i - 1);
+      if (idx < c) break;
+      idx -= c;
+      x++;
+    }
+    m |= 1ull << x;
+    x++;
+  }
+  return m;
+}
+
+// ================================================== option generators
+// build_options / get_builds (agent_functions.py:108-130)
+template <class S>
+CIT_HD bool gen_builds(const CitGame& g, int a, S& s) {
+  const CitPlayer& P = g.pl[a];
+  int lim = P.role == R_ARCHITECT ? 3 : P.role == R_SCHOLAR ? 2 : (P.role == R_BISHOP || P.role == R_NAVIGATOR) ? 0 : 1;
+  int done = g.gs_adm[ADM_NON_TRADE] + (P.role == R_TRADER ? 0 : g.gs_adm[ADM_TRADE]);
+  if (done >= lim) return false;
+  bool factory = p_has(P, 35);
+  uint64_t seen = 0;
+  for (int i = 0; i < P.n_hand; i++) {
+    int c = P.hand[i], t = card_type(c);
+    int cost = card_cost(c) + (factory && card_suit(c) == SUIT_UNIQUE ? 1 : 0);
+    int rep = (p_has(P, t) && !P.replicas) ? P.replicas + 1 : 0;
+    if (cost <= P.gold && !((seen >> t) & 1)) {
+      seen |= 1ull << t;
+      EMIT(mk(O_BUILD, a, -1, c, 0, rep));
+    }
+  }
+  return false;
+}
+
+template <class S>
+CIT_HD bool gen_emperor(const CitGame& g, int a, bool dead, S& s) {   // agent_functions.py:368-382
+  for (int p = 0; p < CIT_NP; p++) {
+    if (p == a) continue;
+    const CitPlayer& Q = g.pl[p];
+    if (Q.n_hand && !dead) EMIT(mk(O_GIVE_CROWN, a, p, 0));
+    if (Q.gold && !dead) EMIT(mk(O_GIVE_CROWN, a, p, 1));
+    if ((!Q.gold && !Q.n_hand) || dead) EMIT(mk(O_GIVE_CROWN, a, p, 2));
+  }
+  return false;
+}
+
+// character_options' per-role generators (agent_functions.py:156-504)
+template <class S>
+CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
+  const CitPlayer& P = g.pl[a];
+  switch (P.role) {
+    case R_ASSASSIN:
+      for (int r = 1; r < 8; r++) EMIT(mk(O_ASSASSINATION, a, -1, r));
+      return false;
+    case R_MAGISTRATE:
+      for (int r = 1; r < 8; r++)
+        for (int f0 = 1; f0 < 8; f0++)
+          for (int f1 = f0 + 1; f1 < 8; f1++)
+            if (r != f0 && r != f1) EMIT(mk(O_MAGISTRATE_WARRANT, a, -1, r, f0, f1));
+      return false;
+    case R_THIEF:
+      for (int r = 2; r < 8; r++) EMIT(mk(O_STEAL, a, -1, r));
+      return false;
+    case R_BLACKMAILER: {
+      uint8_t t = 0xFC;   // ranks 2..7
+      for (int r = 0; r < 8; r++)
+        if (g.rp[r] & RP_POSSESSED) {
+          if (!((t >> r) & 1)) { s.err |= CIT_ERR_VALUE; return true; }
+          t &= (uint8_t)~(1u << r);
+        }
+      for (int x = 0; x < 8; x++)
+        for (int y = x + 1; y < 8; y++)
+          if (((t >> x) & 1) && ((t >> y) & 1)) {
+            EMIT(mk(O_BLACKMAIL, a, -1, x, y));
+            EMIT(mk(O_BLACKMAIL, a, -1, y, x));
+          }
+      return false;
+    }
+    case R_SPY:
+      for (int p = 0; p < CIT_NP; p++)
+        if (p != a)
+          for (int su = 0; su < 5; su++) EMIT(mk(O_SPY, a, p, su));
+      return false;
+    case R_MAGICIAN: {
+      for (int p = 0; p < CIT_NP; p++)
+        if (p != a) EMIT(mk(O_MAGIC_HAND_CHANGE, a, p));
+      int n = P.n_hand;
+      for (int r = 1; r <= n; r++) {
+        long C = binom(n, r), st = subsample_stride(C);
+        int cnt = (int)((C + st - 1) / st);
+        if (s.block(cnt, [&](int i) { return mk(O_DISCARD_AND_DRAW, a, -1, r, 0, 0, 0, unrank_comb(n, r, (long)i * st)); }))
+          return true;
+      }
+      return false;
+    }
+    case R_WIZARD:
+      for (int p = 0; p < CIT_NP; p++)
+        if (p != a && g.pl[p].n_hand > 0) EMIT(mk(O_LOOK_AT_HAND, a, p));
+      return false;
+    case R_SEER:
+      EMIT(mk(O_SEER, a));
+      return false;
+    case R_KING:
+      EMIT(mk(O_TAKE_CROWN_KING, a));
+      return false;
+    case R_EMPEROR:
+      return gen_emperor(g, a, false, s);
+    case R_PATRICIAN:
+      EMIT(mk(O_TAKE_CROWN_PAT, a));
+      return false;
+    case R_BISHOP:
+      EMIT(mk(O_BISHOP, a));
+      return false;
+    case R_CARDINAL: {
+      bool factory_owned = p_has(P, 35);
+      int n = P.n_hand;
+      for (int p = 0; p < CIT_NP; p++) {
+        const CitPlayer& Q = g.pl[p];
+        for (int i = 0; i < n; i++) {
+          int c = P.hand[i], t = card_type(c);
+          int cost = card_cost(c);
+          bool factory = false;
+          if (factory_owned && card_suit(c) == SUIT_UNIQUE) { cost += 1; factory = true; }
+          int rep = (p_has(P, t) && !P.replicas) ? P.replicas + 1 : 0;
+          if (cost > Q.gold) continue;
+          int k = Q.gold - cost;
+          if (k < 0) k = 0;
+          if (n - 1 < k) continue;
+          uint8_t slot[CIT_HAND_CAP];
+          int m = 0;
+          for (int j = 0; j < n; j++)
+            if (card_type(P.hand[j]) != t) slot[m++] = (uint8_t)j;
+          long C = binom(m, k), st = subsample_stride(C);
+          int cnt = (int)((C + st - 1) / st);
+          if (s.block(cnt, [&](int ii) {
+                uint64_t cm = unrank_comb(m, k, (long)ii * st), hm = 0;
+                for (int q = 0; q < m; q++)
+                  if ((cm >> q) & 1) hm |= 1ull << slot[q];
+                return mk(O_CARDINAL, a, p, c, k, rep, factory ? OF_FACTORY : 0, hm);
+              }))
+            return true;
+        }
+      }
+      return false;
+    }
+    case R_ABBOT: {
+      int n = count_suit(P.hand, P.n_hand, SUIT_RELIGION);
+      for (int j = 0; n > 0 && j <= n; j++) EMIT(mk(O_ABBOT_GOLD_OR_CARD, a, -1, n, j));
+      return false;
+    }
+    case R_MERCHANT:
+      EMIT(mk(O_MERCHANT, a));
+      return false;
+    case R_TRADER:
+      EMIT(mk(O_TRADER, a));
+      return false;
+    case R_ARCHITECT:
+      EMIT(mk(O_ARCHITECT, a));
+      return false;
+    case R_NAVIGATOR:
+      EMIT(mk(O_NAVIGATOR, a, -1, 0));
+      EMIT(mk(O_NAVIGATOR, a, -1, 1));
+      return false;
+    case R_SCHOLAR:
+      if (g.n_deck) EMIT(mk(O_SCHOLAR, a));
+      return false;
+    case R_WARLORD:
+      for (int p = 0; p < CIT_NP; p++) {
+        const CitPlayer& Q = g.pl[p];
+        if (Q.n_build >= 7 || Q.role == R_BISHOP) continue;
+        uint64_t seen = 0;
+        for (int i = 0; i < Q.n_build; i++) {
+          int b = Q.build[i], t = card_type(b);
+          if (card_cost(b) - 1 <= P.gold && t != 17 && !((seen >> t) & 1)) {
+            seen |= 1ull << t;
+            EMIT(mk(O_WARLORD, a, p, b));
+          }
+        }
+      }
+      return false;
+    case R_MARSHAL:
+      for (int p = 0; p < CIT_NP; p++) {
+        const CitPlayer& Q = g.pl[p];
+        if (p == a || Q.n_build >= 7 || Q.role == R_BISHOP) continue;
+        uint64_t seen = 0;
+        for (int i = 0; i < Q.n_build; i++) {
+          int b = Q.build[i], t = card_type(b);
+          if (card_cost(b) <= P.gold && card_cost(b) <= 3 && !p_has(P, t) && t != 17 && !((seen >> t) & 1)) {
+            seen |= 1ull << t;
+            EMIT(mk(O_MARSHAL, a, p, b));
+          }
+        }
+      }
+      return false;
+    case R_DIPLOMAT:
+      for (int p = 0; p < CIT_NP; p++) {
+        const CitPlayer& Q = g.pl[p];
+        if (p == a || Q.n_build >= 7 || Q.role == R_BISHOP) continue;
+        uint64_t seen_e = 0;
+        for (int i = 0; i < Q.n_build; i++) {
+          int e = Q.build[i], te = card_type(e);
+          if (te == 17 || p_has(P, te)) continue;   // whole row fails the condition
+          bool dup_e = (seen_e >> te) & 1;
+          seen_e |= 1ull << te;
+          if (dup_e) continue;
+          uint64_t seen_o = 0;
+          for (int j = 0; j < P.n_build; j++) {
+            int own = P.build[j], to = card_type(own);
+            int diff = card_cost(e) - card_cost(own);
+            if (diff <= P.gold && !((seen_o >> to) & 1)) {
+              seen_o |= 1ull << to;
+              EMIT(mk(O_DIPLOMAT, a, p, e, own, diff < 0 ? -diff : diff));
+            }
+          }
+        }
+      }
+      return false;
+    default:
+      return false;   // Witch (handled earlier), Alchemist, rank-8 roles: no character options
+  }
+}
+
+// main_round_options (agent_functions.py:133-147)
+template <class S>
+CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
+  const CitPlayer& P = g.pl[a];
+  if (gen_builds(g, a, s)) return true;
+  if (!g.gs_adm[ADM_ABILITY])
+    if (gen_role(g, a, s)) return true;
+  if (P.role == R_ABBOT && !g.gs_adm[ADM_BEGGED]) EMIT(mk(O_ABBOT_BEG, a));
+  if ((P.role == R_WARLORD || P.role == R_MARSHAL || P.role == R_DIPLOMAT) && !g.gs_adm[ADM_TAKE_GOLD])
+    EMIT(mk(O_TAKE_GOLD_WAR, a));
+  if (p_has(P, 21) && P.gold >= 2 && !g.gs_adm[ADM_SMITHY]) EMIT(mk(O_SMITHY, a));
+  if (p_has(P, 22) && !g.gs_adm[ADM_LAB])
+    for (int i = 0; i < P.n_hand; i++) EMIT(mk(O_LAB, a, -1, P.hand[i]));
+  if (!g.gs_adm[ADM_MAGIC_SCHOOL] && p_has(P, 25))
+    for (int su = 0; su < 5; su++) EMIT(mk(O_MAGIC_SCHOOL, a, -1, su));
+  if (p_has(P, 27))
+    for (int p = 0; p < CIT_NP; p++)
+      if (p != a)
+        for (int i = 0; i < g.pl[p].n_build; i++) EMIT(mk(O_WEAPON_STORAGE, a, p, g.pl[p].build[i]));
+  if (p_has(P, 29) && (P.flags & PF_LIGHTHOUSE)) {
+    uint64_t seen = 0;
+    for (int i = 0; i < g.n_deck; i++) {
+      int c = deck_at(g, i), t = card_type(c);
+      if (!((seen >> t) & 1)) {
+        seen |= 1ull << t;
+        EMIT(mk(O_LIGHTHOUSE, a, -1, c));
+      }
+    }
+  }
+  if (p_has(P, 34) && !g.gs_adm[ADM_MUSEUM]) {
+    uint64_t seen = 0;
+    for (int i = 0; i < P.n_hand; i++) {
+      int c = P.hand[i], t = card_type(c);
+      if (!((seen >> t) & 1)) {
+        seen |= 1ull << t;
+        EMIT(mk(O_MUSEUM, a, -1, c));
+      }
+    }
+  }
+  EMIT(mk(O_FINISH_ROUND, a));
+  return false;
+}
+
+// wizard_take_from_hand_options (agent_functions.py:310-326)
+template <class S>
+CIT_HD bool gen_wizard_take(const CitGame& g, int a, S& s) {
+  const CitPlayer& P = g.pl[a];
+  int e = -1, off = 0, o = 0;
+  for (int i = 0; i < g.n_kh; i++) {
+    const CitKH& k = g.kh[i];
+    if (k.owner == a && kh_conf(k) == 5 && k.target != -1 && (k.conf_flags & 0x10)) { e = i; off = o; break; }
+    o += k.len;
+  }
+  if (e < 0) { s.err |= CIT_ERR_ATTR; return true; }
+  int tgt = g.kh[e].target;
+  bool factory = p_has(P, 35);
+  int rep = 0;
+  uint64_t seen_take = 0, seen_b0 = 0, seen_b1 = 0;
+  int emitted = 0;
+  for (int i = 0; i < g.kh[e].len; i++) {
+    int c = g.kh_pool[off + i], t = card_type(c);
+    if (!((seen_take >> t) & 1)) {
+      seen_take |= 1ull << t;
+      emitted++;
+      EMIT(mk(O_TAKE_FROM_HAND, a, tgt, c, 0, 0, 0));
+    }
+    int cost = card_cost(c) + (factory && card_suit(c) == SUIT_UNIQUE ? 1 : 0);
+    if (p_has(P, t)) rep = P.replicas + 1;
+    uint64_t& seen = rep == 0 ? seen_b0 : seen_b1;   // rep takes at most one non-zero value
+    if (cost <= P.gold && !((seen >> t) & 1)) {
+      seen |= 1ull << t;
+      emitted++;
+      EMIT(mk(O_TAKE_FROM_HAND, a, tgt, c, 0, rep, OF_BUILD));
+    }
+  }
+  if (!emitted) EMIT(mk(O_EMPTY, a, -1, 1));
+  return false;
+}
+
+// get_options dispatcher (agent.py:50-83) on a prepared game.
+template <class S>
+CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
+  int a = g.gs_pid;
+  if (a < 0 || a >= CIT_NP) { s.err |= CIT_ERR_UNSUPPORTED; return true; }
+  const CitPlayer& P = g.pl[a];
+  int st = g.gs_state;
+  if (st == 0) {
+    for (int r = 0; r < 8; r++)
+      if ((g.rtc >> r) & 1) EMIT(mk(O_ROLE_PICK, a, -1, r));
+    return false;
+  }
+  int role = P.role;
+  bool crown = role == R_KING || role == R_PATRICIAN;
+  bool bew = role == ROLE_BEWITCHED;
+  if (!bew && role >= 27) { s.err |= CIT_ERR_KEY; return true; }
+  int rk = bew ? -1 : role / 3;
+  if (bew || !(g.rp[rk] & RP_DEAD)) {
+    switch (st) {
+      case 1:
+        EMIT(mk(O_GOLD_OR_CARD, a, -1, 0));
+        if (g.n_deck > 1) EMIT(mk(O_GOLD_OR_CARD, a, -1, 1));
+        return false;
+      case 2:
+        if (p_has(P, 20)) {
+          for (int i = 0; i < P.n_jd; i++)
+            for (int j = i + 1; j < P.n_jd; j++) EMIT(mk(O_WHICH_CARD, a, -1, P.jd[i], P.jd[j], 0, OF_TUPLE));
+        } else {
+          uint64_t seen = 0;
+          for (int i = 0; i < P.n_jd; i++) {
+            int t = card_type(P.jd[i]);
+            if (!((seen >> t) & 1)) {
+              seen |= 1ull << t;
+              EMIT(mk(O_WHICH_CARD, a, -1, P.jd[i], CIT_NO_CARD));
+            }
+          }
+        }
+        return false;
+      case 3:
+        if (bew) { s.err |= CIT_ERR_KEY; return true; }
+        if (rp_blackmail(g.rp[rk])) {
+          EMIT(mk(O_BLACKMAIL_RESPONSE, a, -1, 0));
+          EMIT(mk(O_BLACKMAIL_RESPONSE, a, -1, 1));
+        } else {
+          EMIT(mk(O_EMPTY, a, -1, 0));
+        }
+        return false;
+      case 4:
+      case 7:
+        if (!g.nx_valid) { s.err |= CIT_ERR_ATTR; return true; }
+        EMIT(mk(st == 4 ? O_REVEAL_BLACKMAIL : O_REVEAL_WARRANT, a, g.nx_pid, 0));
+        EMIT(mk(st == 4 ? O_REVEAL_BLACKMAIL : O_REVEAL_WARRANT, a, g.nx_pid, 1));
+        return false;
+      case 6:
+        if (P.gold > 0) EMIT(mk(O_GRAVEYARD, a));
+        else EMIT(mk(O_EMPTY, a, -1, 1));
+        return false;
+      default:
+        break;
+    }
+    if (role == R_WITCH) {
+      for (int r = 1; r < 8; r++) EMIT(mk(O_BEWITCHING, a, -1, r));
+      return false;
+    }
+    if (bew) { s.err |= CIT_ERR_KEY; return true; }
+    if (!(g.rp[rk] & RP_POSSESSED)) {
+      switch (st) {
+        case 5:
+          return gen_main(g, a, s);
+        case 8: {
+          // seer_give_back_card: the permutations were drawn by cit_prepare_options
+          if (!seer) { s.err |= CIT_ERR_UNSUPPORTED; return true; }
+          int k = g.n_seer == 255 ? 0 : g.n_seer;
+          int cnt = k * P.n_hand * 3;
+          if (s.block(cnt, [&](int i) {
+                uint64_t v = seer[i];
+                return mk(O_GIVE_BACK_CARD, a, -1, 0, (int)(v >> 56), 0, 0, v & 0x00FFFFFFFFFFFFFFull);
+              }))
+            return true;
+          return false;
+        }
+        case 9:
+          for (int i = 0; i < g.n_sch; i++) EMIT(mk(O_SCHOLAR_PICK, a, -1, g.sch[i]));
+          return false;
+        case 10:
+          return gen_wizard_take(g, a, s);
+        default:
+          s.err |= CIT_ERR_NONE_OPTIONS;
+          return true;
+      }
+    }
+    EMIT(mk(O_FINISH_ROUND, a, -1, 0, 0, 0, OF_NEXT_WITCH | (crown ? OF_CROWN : 0)));
+    return false;
+  }
+  if (role == R_EMPEROR && !g.gs_adm[ADM_ABILITY]) return gen_emperor(g, a, true, s);
+  EMIT(mk(O_FINISH_ROUND, a, -1, 0, 0, 0, crown ? OF_CROWN : 0));
+  return false;
+}
+
+// The mutating half of get_options:
+//  * state 9: the scholar's iterate-while-remove over the shared seven-drawn
+//    list (agent_functions.py:462-470);
+//  * state 8: seer_give_back_card's shuffles (agent_functions.py:332-361),
+//    which consume the game's CPython stream inside get_options; the drawn
+//    permutations go to `seer` (CIT_SEER_MAX packed options per lane:
+//    card i in byte i, handout count in byte 7).
+#define CIT_SEER_MAX (5 * CIT_HAND_CAP * 3)
+CIT_HD void cit_prepare_options(CitGame& g, const CitMT& rng, uint64_t* seer) {
+  g.n_sch = 0;
+  if ((g.gs_state != 9 && g.gs_state != 8) || g.gs_pid < 0) return;
+  const CitPlayer& P = g.pl[g.gs_pid];
+  if (P.role >= 27) return;    // the dispatcher reports the error
+  if (P.role == R_WITCH || (g.rp[P.role / 3] & (RP_DEAD | RP_POSSESSED))) return;
+  if (g.gs_state == 8) {
+    if (!seer) return;         // the enumerator reports UNSUPPORTED
+    int k = g.n_seer == 255 ? 0 : g.n_seer;
+    int n = P.n_hand, o = 0;
+    for (int pos = 0; pos < k; pos++) {
+      for (int j = 0; j < n; j++) {
+        int card = P.hand[j], t = card_type(card);
+        uint8_t rest[CIT_HAND_CAP];
+        int m = 0;
+        for (int q = 0; q < n; q++)
+          if (card_type(P.hand[q]) != t) rest[m++] = P.hand[q];
+        for (int rep = 0; rep < 3; rep++) {
+          shuffle_arr(rng, rest, m);
+          // perm = rest[:k-1]; perm.insert(pos, card)  (list.insert clamps pos)
+          uint8_t perm[6];
+          int take = k - 1 < m ? k - 1 : m, len = 0;
+          int ins = pos < take ? pos : take;
+          for (int q = 0; q < take; q++) {
+            if (q == ins) perm[len++] = (uint8_t)card;
+            perm[len++] = rest[q];
+          }
+          if (ins == take) perm[len++] = (uint8_t)card;
+          int h = len < k ? len : k;
+          uint64_t v = (uint64_t)h << 56;
+          for (int q = 0; q < h; q++) v |= (uint64_t)perm[q] << (8 * q);
+          seer[o++] = v;
+        }
+      }
+    }
+    return;
+  }
+  if (g.seven_kind != 1) { g.err |= CIT_ERR_ATTR; return; }
+  int i = 0;
+  while (i < g.n_seven) {
+    int c = g.seven[i];
+    take_like(g.seven, g.n_seven, c);
+    g.sch[g.n_sch++] = (uint8_t)c;
+    i++;
+  }
+}
+
+CIT_HD int cit_count_options(const CitGame& g, uint32_t& err, const uint64_t* seer) {
+  CountSink s;
+  cit_enum_options(g, s, seer);
+  err |= s.err;
+  return s.n;
+}
+CIT_HD CitOpt cit_pick_option(const CitGame& g, int k, const uint64_t* seer) {
+  PickSink s(k);
+  cit_enum_options(g, s, seer);
+  return s.out;
+}
+
+// ====================================================== transitions
+// confirm_role_knowledges (option_functions.py:608-622); the unconfirmed-entry
+// filter keeps every entry (the entry named like the revealed role has id
+// == its rank, never below it), so only the revealed column changes.
+CIT_HD void confirm_roles(CitGame& g, int q) {
+  int rq = role_rank(g, g.pl[q].role);
+  uint16_t v = (uint16_t)((1u << (rq + 1)) | KR_CONFIRMED);
+  for (int p = 0; p < CIT_NP; p++) g.pl[p].kr[q] = v;
+}
+// move_crown + troneroom_owner_gold (option_functions.py:588-595,625-631)
+CIT_HD void move_crown(CitGame& g, int t) {
+  for (int p = 0; p < CIT_NP; p++)
+    if (g.pl[p].flags & PF_CROWN) { g.pl[p].flags &= (uint8_t)~PF_CROWN; break; }
+  g.pl[t].flags |= PF_CROWN;
+  for (int p = 0; p < CIT_NP; p++)
+    if (p_has(g.pl[p], 32)) { g.pl[p].gold++; break; }
+}
+// carry_out_building (option_functions.py:102-127)
+CIT_HD void do_build(CitGame& g, int a, int card, int replica) {
+  CitPlayer& P = g.pl[a];
+  put_card(g, BUILD(P), take_like(P.hand, P.n_hand, card));
+  if (P.role != R_ALCHEMIST) P.gold = (int16_t)(P.gold - card_cost(card));
+  if (replica) P.replicas = (int8_t)replica;
+  gs_append(g, card_suit(card) == SUIT_TRADE ? ADM_TRADE : ADM_NON_TRADE);
+  if (card_type(card) == 29) P.flags |= PF_LIGHTHOUSE;
+  if (rp_warrant(rp_of(g, P.role)) == WB_NONE) {
+    at5(g, a, -1);
+  } else {
+    g.warrant = (uint8_t)card;
+    gs_set(g, 7, holder_checked(g, 0));
+    g.gs_intr = 1;
+    gs_make_next(g, a, NX_ALIAS);
+  }
+}
+// check_if_building_is_replica + settle_museum + settle_lighthouse (:573-606)
+CIT_HD void settle(CitGame& g, int name, int a, int t, int card) {
+  CitPlayer& P = g.pl[a];
+  CitPlayer& T = g.pl[t];
+  int ty = card_type(card);
+  if (count_type(T.build, T.n_build, ty) > 1) T.replicas = (int8_t)(T.replicas - 1);
+  if (ty == 34) {
+    int n = T.n_museum;
+    for (int i = 0; i < n; i++) {
+      int c = pop_front(T.museum, T.n_museum);
+      if (name == O_WARLORD) put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, c);
+      else put_card(g, MUSEUM(P), c);
+    }
+  }
+  if (ty == 29 && (T.flags & PF_LIGHTHOUSE)) {
+    T.flags &= (uint8_t)~PF_LIGHTHOUSE;
+    P.flags |= PF_LIGHTHOUSE;
+  }
+}
+
+// finish_main_sequnce_actions (option_functions.py:189-243); returns winner or -1
+CIT_HD int do_finish(CitGame& g, const CitOpt& o, const CitMT& rng) {
+  int a = o.perp;
+  CitPlayer& P = g.pl[a];
+  bool dead = rp_of(g, P.role) & RP_DEAD;
+  if (g.err) return -1;
+  if (!dead) {
+    if (p_has(P, 28) && P.n_hand == 0) draw_into(g, rng, JD(P), 2);
+    if (p_has(P, 30) && P.n_hand == 0) P.gold++;
+  }
+  if (o.flags & OF_CROWN) {
+    confirm_roles(g, a);
+    move_crown(g, a);
+  } else if (rp_of(g, P.role) & RP_DEAD) {
+    confirm_roles(g, a);
+  }
+  if (o.flags & OF_NEXT_WITCH) {
+    int w = holder_checked(g, 0);
+    gs_set(g, 5, w);
+    g.pl[w].role = P.role;
+    rp_of(g, P.role) &= (uint8_t)~RP_POSSESSED;
+    P.role = ROLE_BEWITCHED;
+    int wr = role_rank(g, g.pl[w].role);
+    for (int p = 0; p < CIT_NP; p++) {
+      if (p != w) g.pl[p].kr[w] = (uint16_t)((g.pl[p].kr[w] & KR_CONFIRMED) | (1u << (wr + 1)));
+      if (p != a) g.pl[p].kr[a] = (uint16_t)((g.pl[p].kr[a] & KR_CONFIRMED) | 1u);
+    }
+    gs_rebind_adm(g);
+    return -1;
+  }
+  if (g.n_used_roles == 0 || g.n_used_roles == 255) { g.err |= CIT_ERR_INDEX; return -1; }
+  if (g.used_roles[g.n_used_roles - 1] == role_rank(g, P.role)) {
+    int w = check_game_ending(g);
+    if (w < 0) cit_setup_round(g, rng);
+    return w;
+  }
+  setup_next_player(g, a);
+  return -1;
+}
+
+// option.carry_out (option.py:118-122): transition then is_last_round.
+// Returns the winner's index, or -1.
+CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, const CitMT& rng) {
+  int a = o.perp;
+  CitPlayer& P = g.pl[a];
+  int w = -1;
+  switch (o.name) {
+    case O_ROLE_PICK: {                                      // :6-30
+      int rk = o.a;
+      P.role = g.roles[rk];
+      g.rtc &= (uint8_t)~(1u << rk);
+      uint16_t rtc_mask = (uint16_t)(g.rtc << 1);
+      uint16_t before = (uint16_t)(0x1FE & ~rtc_mask & ~(1u << (rk + 1)));
+      int pos_a = 0;
+      for (int i = 0; i < CIT_NP; i++)
+        if (g.turn[i] == a) pos_a = i;
+      for (int i = 0; i < CIT_NP; i++) {
+        int p = g.turn[i];
+        if (p == a) continue;
+        P.kr[p] = (uint16_t)((P.kr[p] & KR_CONFIRMED) | (i < pos_a ? before : rtc_mask));
+      }
+      if (a != g.turn[CIT_NP - 1]) gs_set(g, 0, g.turn[pos_a + 1]);
+      else setup_next_player(g, -1);
+      break;
+    }
+    case O_GOLD_OR_CARD: {                                   // :33-55
+      confirm_roles(g, a);
+      if (rp_of(g, P.role) & RP_ROBBED) {
+        int th = holder_checked(g, 1);
+        g.pl[th].gold = (int16_t)(g.pl[th].gold + P.gold);
+        P.gold = 0;
+      }
+      if (o.a == 0) {
+        P.gold += 2;
+        gs_set(g, 3, a);
+      } else {
+        draw_into(g, rng, JD(P), p_has(P, 16) ? 3 : 2);
+        gs_set(g, 2, a);
+      }
+      break;
+    }
+    case O_WHICH_CARD: {                                     // :58-66
+      put_card(g, HAND(P), take_like(P.jd, P.n_jd, o.a));
+      if (o.b != CIT_NO_CARD) put_card(g, HAND(P), take_like(P.jd, P.n_jd, o.b));
+      for (int i = 0; i < P.n_jd; i++) deck_put(g, P.jd[i]);
+      P.n_jd = 0;
+      gs_set(g, 3, a);
+      break;
+    }
+    case O_BLACKMAIL_RESPONSE: {                             // :71-82
+      if (o.a == 0) {
+        int bm = holder_checked(g, 1);
+        g.pl[bm].gold = (int16_t)(g.pl[bm].gold + P.gold / 2);
+        P.gold = (int16_t)(P.gold - P.gold / 2);
+        gs_set(g, 5, a);
+      } else {
+        gs_set(g, 4, holder_checked(g, 1));
+        g.gs_intr = 1;
+        gs_make_next(g, a, NX_FRESH);
+      }
+      break;
+    }
+    case O_REVEAL_BLACKMAIL: {                               // :85-92
+      CitPlayer& T = g.pl[o.target];
+      if (o.a == 0 && rp_blackmail(rp_of(g, T.role)) == WB_REAL) {
+        P.gold = (int16_t)(P.gold + T.gold);
+        T.gold = 0;
+        for (int r = 0; r < 8; r++) g.rp[r] &= (uint8_t)~(3u << RP_BLACKMAIL_SHIFT);
+      }
+      gs_goto_next(g);
+      break;
+    }
+    case O_REVEAL_WARRANT: {                                 // :94-100
+      CitPlayer& T = g.pl[o.target];
+      if (o.a == 0 && rp_warrant(rp_of(g, T.role)) == WB_REAL) {
+        if (g.warrant == CIT_NO_CARD) { g.err |= CIT_ERR_ATTR; break; }
+        put_card(g, BUILD(P), take_like(T.build, T.n_build, g.warrant));
+        T.gold = (int16_t)(T.gold + card_cost(g.warrant));
+        for (int r = 0; r < 8; r++) g.rp[r] &= (uint8_t)~(3u << RP_WARRANT_SHIFT);
+      }
+      gs_goto_next(g);
+      break;
+    }
+    case O_BUILD:
+      do_build(g, a, o.a, (int8_t)o.c);
+      break;
+    case O_EMPTY:                                            // :68-69
+      if (o.a == 0) gs_fresh(g, 5, a);
+      else gs_goto_next(g);
+      break;
+    case O_FINISH_ROUND:
+      w = do_finish(g, o, rng);
+      break;
+    case O_SMITHY:                                           // :131-138
+      P.gold -= 2;
+      draw_into(g, rng, JD(P), 3);
+      at5(g, a, ADM_SMITHY);
+      break;
+    case O_LAB:                                              // :140-145
+      put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, take_like(P.hand, P.n_hand, o.a));
+      P.gold++;
+      at5(g, a, ADM_LAB);
+      break;
+    case O_MAGIC_SCHOOL:                                     // :147-153
+      take_like(P.build, P.n_build, 25);
+      put_card(g, BUILD(P), o.a == SUIT_UNIQUE ? 25 : 40 + o.a);
+      at5(g, a, ADM_MAGIC_SCHOOL);
+      break;
+    case O_WEAPON_STORAGE: {                                 // :167-171
+      CitPlayer& T = g.pl[o.target];
+      put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, take_like(P.build, P.n_build, 27));
+      put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, take_like(T.build, T.n_build, o.a));
+      at5(g, a, -1);
+      break;
+    }
+    case O_LIGHTHOUSE:                                       // :173-180
+      kh_append(g, a, -1, 5, false, g.n_deck, [&g](int i) { return deck_at(g, i); });
+      put_card(g, HAND(P), deck_take_like(g, o.a));
+      P.flags &= (uint8_t)~PF_LIGHTHOUSE;
+      deck_shuffle(g, rng);
+      at5(g, a, -1);
+      break;
+    case O_MUSEUM:                                           // :161-165
+      put_card(g, MUSEUM(P), take_like(P.hand, P.n_hand, o.a));
+      at5(g, a, ADM_MUSEUM);
+      break;
+    case O_GRAVEYARD:                                        // :183-187
+      if (!g.n_discard) { g.err |= CIT_ERR_INDEX; break; }
+      put_card(g, BUILD(P), g.discard[--g.n_discard]);
+      P.gold--;
+      gs_goto_next(g);
+      break;
+    case O_TAKE_GOLD_WAR:                                    // :553-559
+      P.gold = (int16_t)(P.gold + count_suit(P.build, P.n_build, SUIT_WAR));
+      at5(g, a, ADM_TAKE_GOLD);
+      break;
+    case O_ASSASSINATION:                                    // :245-249
+      g.rp[o.a] |= RP_DEAD;
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_MAGISTRATE_WARRANT:                               // :251-257
+      g.rp[o.a] = (uint8_t)((g.rp[o.a] & ~(3u << RP_WARRANT_SHIFT)) | (WB_REAL << RP_WARRANT_SHIFT));
+      g.rp[o.b] = (uint8_t)((g.rp[o.b] & ~(3u << RP_WARRANT_SHIFT)) | (WB_FAKE << RP_WARRANT_SHIFT));
+      g.rp[o.c] = (uint8_t)((g.rp[o.c] & ~(3u << RP_WARRANT_SHIFT)) | (WB_FAKE << RP_WARRANT_SHIFT));
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_BEWITCHING:                                       // :259-262
+      g.rp[o.a] |= RP_POSSESSED;
+      P.flags |= PF_WITCH;
+      setup_next_player(g, a);
+      break;
+    case O_STEAL:                                            // :265-269
+      g.rp[o.a] |= RP_ROBBED;
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_BLACKMAIL:                                        // :271-276
+      g.rp[o.a] = (uint8_t)((g.rp[o.a] & ~(3u << RP_BLACKMAIL_SHIFT)) | (WB_REAL << RP_BLACKMAIL_SHIFT));
+      g.rp[o.b] = (uint8_t)((g.rp[o.b] & ~(3u << RP_BLACKMAIL_SHIFT)) | (WB_FAKE << RP_BLACKMAIL_SHIFT));
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_SPY: {                                            // :278-288
+      CitPlayer& T = g.pl[o.target];
+      int n = count_suit(T.hand, T.n_hand, o.a);
+      int steal = n < T.gold ? n : T.gold;
+      P.gold = (int16_t)(P.gold + steal);
+      T.gold = (int16_t)(T.gold - steal);
+      draw_into(g, rng, HAND(P), 1);
+      at5(g, a, ADM_ABILITY);
+      break;
+    }
+    case O_MAGIC_HAND_CHANGE: {                              // :291-303
+      CitPlayer& T = g.pl[o.target];
+      uint8_t tmp[CIT_HAND_CAP];
+      int n = P.n_hand;
+      for (int i = 0; i < n; i++) tmp[i] = P.hand[i];
+      for (int i = 0; i < T.n_hand; i++) P.hand[i] = T.hand[i];
+      P.n_hand = T.n_hand;
+      for (int i = 0; i < n; i++) T.hand[i] = tmp[i];
+      T.n_hand = (uint8_t)n;
+      at5(g, a, ADM_ABILITY);
+      break;
+    }
+    case O_DISCARD_AND_DRAW: {                               // :291-303, iterate-while-remove
+      int i = 0;
+      while (i < P.n_hand) {
+        deck_put(g, take_like(P.hand, P.n_hand, P.hand[i]));
+        i++;
+      }
+      draw_into(g, rng, HAND(P), P.n_hand);
+      at5(g, a, ADM_ABILITY);
+      break;
+    }
+    case O_LOOK_AT_HAND: {                                   // :305-310
+      const CitPlayer& T = g.pl[o.target];
+      kh_append(g, a, o.target, 5, true, T.n_hand, [&T](int i) { return T.hand[i]; });
+      gs_set(g, 10, a);
+      gs_append(g, ADM_ABILITY);
+      gs_make_next(g, a, NX_ALIAS);
+      break;
+    }
+    case O_TAKE_FROM_HAND: {                                 // :312-328
+      CitPlayer& T = g.pl[o.target];
+      int e = -1;
+      for (int i = 0; i < g.n_kh; i++)
+        if (g.kh[i].owner == a && (g.kh[i].conf_flags & 0x10)) { e = i; break; }
+      if (e < 0) { g.err |= CIT_ERR_ATTR; break; }
+      put_card(g, HAND(P), take_like(T.hand, T.n_hand, o.a));
+      if (o.flags & OF_BUILD) {
+        int rep = count_type(P.build, P.n_build, card_type(o.a));   // option.attributes['replica'] is overwritten
+        do_build(g, a, o.a, rep);
+      }
+      kh_take_like(g, e, o.a);
+      gs_goto_next(g);
+      break;
+    }
+    case O_SEER: {                                           // :330-341
+      g.n_seer = 0;
+      for (int p = 0; p < CIT_NP; p++) {
+        CitPlayer& Q = g.pl[p];
+        if (p == a || !Q.n_hand) continue;
+        shuffle_arr(rng, Q.hand, Q.n_hand);
+        reshuffle_if_empty(g, rng);
+        put_card(g, HAND(P), pop_front(Q.hand, Q.n_hand));
+        g.seer_from[g.n_seer++] = (uint8_t)p;
+      }
+      gs_set(g, 8, a);
+      gs_append(g, ADM_ABILITY);
+      gs_make_next(g, a, NX_ALIAS);
+      break;
+    }
+    case O_GIVE_BACK_CARD: {                                 // :343-350
+      int k = o.b;
+      for (int i = 0; i < k; i++) {
+        int pid = g.seer_from[i];
+        int c = (int)((o.x >> (8 * i)) & 0xFF);
+        put_card(g, HAND(g.pl[pid]), take_like(P.hand, P.n_hand, c));
+        kh_append(g, a, pid, 5, false, 1, [c](int) { return c; });
+      }
+      g.n_seer = 0;
+      gs_goto_next(g);
+      break;
+    }
+    case O_TAKE_CROWN_KING:                                  // :354-363
+      P.gold = (int16_t)(P.gold + count_suit(P.build, P.n_build, SUIT_LORD));
+      if (!(P.flags & PF_WITCH)) move_crown(g, a);
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_TAKE_CROWN_PAT: {                                 // :365-375
+      int n = count_suit(P.build, P.n_build, SUIT_LORD);
+      draw_into(g, rng, HAND(P), n);
+      if (!(P.flags & PF_WITCH)) move_crown(g, a);
+      at5(g, a, ADM_ABILITY);
+      break;
+    }
+    case O_GIVE_CROWN: {                                     // :377-393
+      CitPlayer& T = g.pl[o.target];
+      P.gold = (int16_t)(P.gold + count_suit(P.build, P.n_build, SUIT_LORD));
+      if (o.a == 0) {
+        shuffle_arr(rng, T.hand, T.n_hand);
+        put_card(g, HAND(P), pop_front(T.hand, T.n_hand));
+      } else if (o.a == 1) {
+        P.gold++;
+        T.gold--;
+      }
+      confirm_roles(g, a);
+      move_crown(g, o.target);
+      at5(g, a, ADM_ABILITY);
+      break;
+    }
+    case O_BISHOP:                                           // :397-403
+      P.gold = (int16_t)(P.gold + count_suit(P.build, P.n_build, SUIT_RELIGION));
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_CARDINAL: {                                       // :422-439
+      CitPlayer& T = g.pl[o.target];
+      uint8_t give[CIT_HAND_CAP];
+      int ng = 0;
+      for (int i = 0; i < P.n_hand; i++)
+        if ((o.x >> i) & 1) give[ng++] = P.hand[i];
+      put_card(g, BUILD(P), take_like(P.hand, P.n_hand, o.a));
+      P.gold = (int16_t)(P.gold - (card_cost(o.a) - (o.flags & OF_FACTORY ? 1 : 0)));
+      if (P.gold < 0) P.gold = 0;
+      if ((int8_t)o.c) P.replicas = (int8_t)o.c;
+      if (ng) {
+        T.gold = (int16_t)(T.gold - ng);
+        for (int i = 0; i < ng; i++) put_card(g, HAND(T), take_like(P.hand, P.n_hand, give[i]));
+      }
+      at5(g, a, ADM_ABILITY);
+      break;
+    }
+    case O_ABBOT_GOLD_OR_CARD:                               // :405-412
+      P.gold = (int16_t)(P.gold + (o.a - o.b));
+      draw_into(g, rng, HAND(P), o.b);
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_ABBOT_BEG: {                                      // :414-420
+      int best = 0;
+      for (int p = 1; p < CIT_NP; p++)
+        if (g.pl[p].gold > g.pl[best].gold) best = p;
+      g.pl[best].gold--;
+      int ab = holder_checked(g, 4);
+      g.pl[ab].gold++;
+      at5(g, a, ADM_BEGGED);
+      break;
+    }
+    case O_MERCHANT:                                         // :442-449
+      P.gold = (int16_t)(P.gold + count_suit(P.build, P.n_build, SUIT_TRADE) + 1);
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_ALCHEMIST:                                        // :451-452
+      break;
+    case O_TRADER:                                           // :455-461
+      P.gold = (int16_t)(P.gold + count_suit(P.build, P.n_build, SUIT_TRADE));
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_ARCHITECT:                                        // :464-471
+      draw_into(g, rng, HAND(P), 2);
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_NAVIGATOR:                                        // :473-483
+      if (o.a == 1) draw_into(g, rng, HAND(P), 4);
+      else P.gold += 4;
+      at5(g, a, ADM_ABILITY);
+      break;
+    case O_SCHOLAR: {                                        // :485-496
+      g.seven_kind = 1;
+      g.n_seven = 0;
+      int n = g.n_deck < 7 ? g.n_deck : 7;
+      for (int i = 0; i < n; i++) {
+        reshuffle_if_empty(g, rng);
+        int c = deck_draw(g);
+        put_card(g, HAND(P), c);
+        put_card(g, g.seven, g.n_seven, CIT_SEVEN_CAP, c);
+      }
+      gs_set(g, 9, a);
+      gs_append(g, ADM_ABILITY);
+      gs_make_next(g, a, NX_ALIAS);
+      break;
+    }
+    case O_SCHOLAR_PICK:                                     // :498-502
+      for (int i = 0; i < g.n_seven; i++) deck_put(g, take_like(P.hand, P.n_hand, g.seven[i]));
+      gs_goto_next(g);
+      g.seven_kind = 2;
+      g.n_seven = 0;
+      break;
+    case O_WARLORD: {                                        // :517-535
+      CitPlayer& T = g.pl[o.target];
+      P.gold = (int16_t)(P.gold - (card_cost(o.a) - 1));
+      put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, take_like(T.build, T.n_build, o.a));
+      settle(g, O_WARLORD, a, o.target, o.a);
+      at5(g, a, ADM_ABILITY);
+      int owner = -1;
+      for (int p = 0; p < CIT_NP; p++)
+        if (p_has(g.pl[p], 24)) { owner = p; break; }
+      if (owner >= 0 && owner != a) {
+        gs_set(g, 6, owner);
+        g.gs_intr = 1;
+        gs_make_next(g, a, NX_ABILITY);
+      }
+      break;
+    }
+    case O_MARSHAL: {                                        // :505-515
+      CitPlayer& T = g.pl[o.target];
+      P.gold = (int16_t)(P.gold - card_cost(o.a));
+      T.gold = (int16_t)(T.gold + card_cost(o.a));
+      put_card(g, BUILD(P), take_like(T.build, T.n_build, o.a));
+      settle(g, O_MARSHAL, a, o.target, o.a);
+      at5(g, a, ADM_ABILITY);
+      break;
+    }
+    case O_DIPLOMAT: {                                       // :538-551
+      CitPlayer& T = g.pl[o.target];
+      P.gold = (int16_t)(P.gold - o.c);
+      T.gold = (int16_t)(T.gold + o.c);
+      put_card(g, BUILD(P), take_like(T.build, T.n_build, o.a));
+      put_card(g, BUILD(T), take_like(P.build, P.n_build, o.b));
+      settle(g, O_DIPLOMAT, a, o.target, o.a);
+      at5(g, a, ADM_ABILITY);
+      break;
+    }
+    default:
+      g.err |= CIT_ERR_UNSUPPORTED;
+      break;
+  }
+  is_last_round(g);
+  g.steps++;
+  return w;
+}
+
+// One random-policy step (compare_to_random.py:37-39): get_options ->
+// random.choice -> carry_out.  Returns 1 when the lane is done (winner or error).
+CIT_HD int cit_random_step(CitGame& g, const CitMT& rng, uint64_t* seer) {
+  cit_prepare_options(g, rng, seer);
+  uint32_t err = 0;
+  int n = cit_count_options(g, err, seer);
+  if (err) { g.err |= err; return 1; }
+  if (n == 0) { g.err |= CIT_ERR_EMPTY; return 1; }
+  int k = (int)mt_randbelow(rng, (uint32_t)n);
+  CitOpt o = cit_pick_option(g, k, seer);
+  int w = cit_carry_out(g, o, rng);
+  return (w >= 0 || g.err || g.terminal) ? 1 : 0;
+}

@@ -1,0 +1,108 @@
+// TEST-ONLY host build of the engine headers (g++, no HIP).  Loaded by the
+// CPU test suite to check the engine logic against the golden fixtures in
+// this (GPU-less) container.  It is NOT part of the product path: the Python
+// package only ever loads libcitadels_hip.so and has no CPU fallback.
+//
+// Same argument conventions as the HIP C-ABI in include/citadels.h, minus the
+// stream, with host pointers; names are prefixed cith_.
+#include <stddef.h>
+#include <string.h>
+
+#include "cit_engine.h"
+
+extern "C" {
+
+int cith_game_bytes() { return CIT_GAME_BYTES; }
+int cith_sizeof_game() { return (int)sizeof(CitGame); }
+int cith_seer_max() { return CIT_SEER_MAX; }
+
+// field offsets, checked against the Python mirror in layout.py
+int cith_layout(int* out, int n) {
+  int v[] = {(int)sizeof(CitPlayer),
+             (int)offsetof(CitGame, deck),
+             (int)offsetof(CitGame, kh),
+             (int)offsetof(CitGame, roles),
+             (int)offsetof(CitGame, gs_state),
+             (int)offsetof(CitGame, points),
+             (int)offsetof(CitGame, err),
+             (int)offsetof(CitGame, steps),
+             (int)sizeof(CitOpt)};
+  int k = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < k && i < n; i++) out[i] = v[i];
+  return k;
+}
+
+static CitMT lane_rng(uint32_t* mt, uint32_t* idx, int B, int l) {
+  CitMT r;
+  r.mt = mt + l;
+  r.idx = idx + l;
+  r.stride = B;
+  return r;
+}
+
+void cith_mt_seed(uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int numpy_style) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    if (numpy_style) mt_init_genrand(r, (uint32_t)seeds[l]);
+    else mt_seed_cpython(r, seeds[l]);
+  }
+}
+
+void cith_mt_draw(uint32_t* mt, uint32_t* idx, int B, int lane, int n, uint32_t* out) {
+  CitMT r = lane_rng(mt, idx, B, lane);
+  for (int i = 0; i < n; i++) out[i] = mt_next(r);
+}
+
+void cith_mt_randbelow(uint32_t* mt, uint32_t* idx, int B, int lane, uint32_t bound, int n, uint32_t* out) {
+  CitMT r = lane_rng(mt, idx, B, lane);
+  for (int i = 0; i < n; i++) out[i] = mt_randbelow(r, bound);
+}
+
+void cith_mt_random(uint32_t* mt, uint32_t* idx, int B, int lane, int n, double* out) {
+  CitMT r = lane_rng(mt, idx, B, lane);
+  for (int i = 0; i < n; i++) out[i] = mt_random(r);
+}
+
+void cith_init(CitGame* g, uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int preset) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    mt_seed_cpython(r, seeds[l]);
+    cit_init_game(g[l], r, preset != 0);
+  }
+}
+
+void cith_get_options(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, CitOpt* out, int max_opts,
+                      int* n_opts) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    uint64_t* sc = seer + (long)l * CIT_SEER_MAX;
+    cit_prepare_options(g[l], r, sc);
+    ListSink s(out + (long)l * max_opts, max_opts);
+    cit_enum_options(g[l], s, sc);
+    g[l].err |= s.err;
+    n_opts[l] = s.n;
+  }
+}
+
+void cith_carry_out(CitGame* g, uint32_t* mt, uint32_t* idx, int B, const CitOpt* chosen, int* winner) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    winner[l] = cit_carry_out(g[l], chosen[l], r);
+  }
+}
+
+void cith_rollout(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_steps, int* steps,
+                  int* winner) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    int s = 0;
+    while (!g[l].terminal && !g[l].err && (max_steps < 0 || s < max_steps)) {
+      cit_random_step(g[l], r, seer + (long)l * CIT_SEER_MAX);
+      s++;
+    }
+    steps[l] = s;
+    winner[l] = g[l].winner;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,79 @@
+"""ctypes mirror of the packed row layout in csrc/cit_core.h.
+
+`CitGame` rows are CIT_GAME_BYTES wide; tests check `sizeof` and a few field
+offsets against the values the native library reports (cit_layout), so the
+two definitions cannot drift apart silently.
+"""
+import ctypes as C
+
+NP = 6
+HAND_CAP, BUILD_CAP, JD_CAP, MUSEUM_CAP = 32, 16, 24, 16
+DECK_CAP, DISCARD_CAP, USED_CAP = 128, 80, 80
+KH_MAX, KH_POOL, SEVEN_CAP = 32, 252, 8
+GAME_BYTES = 1456
+MT_N = 624
+SEER_MAX = 5 * HAND_CAP * 3      # CIT_SEER_MAX: packed seer give-back options per lane
+NO_CARD = 255
+ROLE_BEWITCHED, ROLE_NONE = 27, 255
+
+ERR_BITS = {
+    0x1: "OverflowError", 0x2: "IndexError", 0x4: "KeyError", 0x8: "ValueError",
+    0x10: "IndexError", 0x20: "AttributeError", 0x40: "NotImplementedError", 0x80: "TypeError",
+}
+
+
+class CitPlayer(C.Structure):
+    _fields_ = [
+        ("hand", C.c_uint8 * HAND_CAP), ("build", C.c_uint8 * BUILD_CAP), ("jd", C.c_uint8 * JD_CAP),
+        ("museum", C.c_uint8 * MUSEUM_CAP),
+        ("n_hand", C.c_uint8), ("n_build", C.c_uint8), ("n_jd", C.c_uint8), ("n_museum", C.c_uint8),
+        ("gold", C.c_int16), ("role", C.c_uint8), ("replicas", C.c_int8), ("flags", C.c_uint8),
+        ("pad0", C.c_uint8), ("kr", C.c_uint16 * NP), ("pad1", C.c_uint16),
+    ]
+
+
+class CitKH(C.Structure):
+    _fields_ = [("owner", C.c_uint8), ("target", C.c_int8), ("conf_flags", C.c_uint8), ("len", C.c_uint8)]
+
+
+class CitGame(C.Structure):
+    _fields_ = [
+        ("pl", CitPlayer * NP),
+        ("deck", C.c_uint8 * DECK_CAP), ("discard", C.c_uint8 * DISCARD_CAP),
+        ("used_cards", C.c_uint8 * USED_CAP), ("kh_pool", C.c_uint8 * KH_POOL), ("kh", CitKH * KH_MAX),
+        ("deck_head", C.c_uint8), ("n_deck", C.c_uint8), ("n_discard", C.c_uint8), ("n_used_cards", C.c_uint8),
+        ("n_kh", C.c_uint8), ("kh_fill", C.c_uint8), ("preset", C.c_uint8), ("pad2", C.c_uint8),
+        ("roles", C.c_uint8 * 8), ("rtc", C.c_uint8), ("n_used_roles", C.c_uint8),
+        ("used_roles", C.c_int8 * NP), ("turn", C.c_uint8 * NP), ("rp", C.c_uint8 * 8),
+        ("gs_state", C.c_uint8), ("gs_pid", C.c_int8), ("gs_adm", C.c_uint8 * 9), ("gs_intr", C.c_uint8),
+        ("nx_valid", C.c_uint8), ("nx_state", C.c_uint8), ("nx_pid", C.c_int8), ("nx_adm", C.c_uint8 * 9),
+        ("nx_intr", C.c_uint8), ("nx_alias", C.c_uint8), ("nx_hasnext", C.c_uint8),
+        ("ending", C.c_uint8), ("terminal", C.c_uint8), ("winner", C.c_int8), ("has_points", C.c_uint8),
+        ("points", C.c_int16 * NP), ("warrant", C.c_uint8), ("n_seer", C.c_uint8), ("seer_from", C.c_uint8 * 5),
+        ("seven_kind", C.c_uint8), ("n_seven", C.c_uint8), ("seven", C.c_uint8 * SEVEN_CAP),
+        ("n_sch", C.c_uint8), ("sch", C.c_uint8 * SEVEN_CAP),
+        ("err", C.c_uint32), ("steps", C.c_uint32),
+    ]
+
+
+class CitOpt(C.Structure):
+    _fields_ = [("name", C.c_uint8), ("perp", C.c_uint8), ("target", C.c_int8), ("a", C.c_uint8),
+                ("b", C.c_uint8), ("c", C.c_uint8), ("d", C.c_uint8), ("flags", C.c_uint8), ("x", C.c_uint64)]
+
+
+def expected_layout():
+    """The values cit_layout()/cith_layout() must report (see cit_host.cpp)."""
+    return [C.sizeof(CitPlayer), CitGame.deck.offset, CitGame.kh.offset, CitGame.roles.offset,
+            CitGame.gs_state.offset, CitGame.points.offset, CitGame.err.offset, CitGame.steps.offset,
+            C.sizeof(CitOpt)]
+
+
+def game_from_bytes(b):
+    """A CitGame view over one row (bytes / bytearray / numpy uint8 row)."""
+    buf = bytes(b)
+    assert len(buf) >= C.sizeof(CitGame)
+    return CitGame.from_buffer_copy(buf[:C.sizeof(CitGame)])
+
+
+def opt_from_bytes(b):
+    return CitOpt.from_buffer_copy(bytes(b)[:16])

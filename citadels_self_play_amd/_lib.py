@@ -1,0 +1,63 @@
+"""ctypes binding of libcitadels_hip.so (include/citadels.h).
+
+The library is built in-tree by `__graft_entry__.build()` (hipcc
+--offload-arch=gfx950).  There is no CPU fallback: if the library is missing
+or no GPU is visible, using the engine raises.
+"""
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcitadels_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "citadels.h")
+
+_lib = None
+
+vp, i32, u64 = C.c_void_p, C.c_int, C.c_uint64
+
+_SIGS = {
+    "cit_abi_version": ([], i32),
+    "cit_game_bytes": ([], i32),
+    "cit_seer_scratch_words": ([], i32),
+    "cit_layout": ([vp, i32], i32),
+    "cit_mt_seed": ([vp, vp, i32, vp, i32, vp], i32),
+    "cit_mt_draw": ([vp, vp, i32, i32, vp, vp], i32),
+    "cit_init": ([vp, vp, vp, i32, vp, i32, vp], i32),
+    "cit_get_options": ([vp, vp, vp, vp, i32, vp, i32, vp, vp], i32),
+    "cit_random_choice": ([vp, vp, vp, i32, vp, i32, vp, vp, vp, vp], i32),
+    "cit_carry_out": ([vp, vp, vp, i32, vp, vp, vp], i32),
+    "cit_rollout_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def declared_symbols():
+    """Function names declared in include/citadels.h."""
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\bint\s+(cit_\w+)\s*\(", txt)))
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError("libcitadels_hip.so is not built (run __graft_entry__.build()); "
+                          "the Citadels engine has no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise NativeError("%s failed with code %d" % (what, rc))

@@ -48,6 +48,8 @@
 #define CIT_ERR_ATTR 0x20u         // get_player_from_role_id(..) is None -> AttributeError
 #define CIT_ERR_UNSUPPORTED 0x40u  // a branch this build does not implement
 #define CIT_ERR_NONE_OPTIONS 0x80u // get_options fell through and returned None
+#define CIT_ERR_STEP_CAP 0x100u    // rollout hit its hard step cap (the reference has no cap)
+#define CIT_ROLLOUT_CAP 20000      // max_steps < 0 means "to terminal", bounded by this
 
 // --------------------------------------------------------------- card codes
 // code < 40: type_ID with its table suit; 40..44: Magic School (type 25)

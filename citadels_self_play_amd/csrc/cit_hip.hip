@@ -1,0 +1,263 @@
+// HIP kernels + C ABI (include/citadels.h) of the MI355X Citadels engine.
+//
+// Execution model: one lane = one game.  A workgroup of G lanes stages its G
+// packed rows (CIT_GAME_BYTES each) from HBM into LDS at an odd-dword stride
+// (same-field accesses of different lanes hit different banks), runs the
+// engine on its lane's row in LDS, and writes the rows back.  The CPython
+// MT19937 streams stay in HBM, structure-of-arrays ([624][B]), so the lanes of
+// a wave twisting together read and write consecutive words.
+#include <hip/hip_runtime.h>
+
+#include "../../include/citadels.h"
+#include "cit_engine.h"
+
+static_assert(sizeof(CitOpt) == sizeof(CitOption), "descriptor layouts differ");
+
+#define ROW_W (CIT_GAME_BYTES / 4)
+#define LDS_W (ROW_W + 1)
+#define MAX_G 64
+
+namespace {
+
+__device__ __forceinline__ void stage_in(uint32_t* lds, const uint32_t* __restrict__ gm, long g0, int nrows) {
+  for (int i = threadIdx.x; i < nrows * ROW_W; i += blockDim.x) {
+    int r = i / ROW_W, w = i - r * ROW_W;
+    lds[r * LDS_W + w] = gm[(g0 + r) * ROW_W + w];
+  }
+}
+__device__ __forceinline__ void stage_out(const uint32_t* lds, uint32_t* __restrict__ gm, long g0, int nrows) {
+  for (int i = threadIdx.x; i < nrows * ROW_W; i += blockDim.x) {
+    int r = i / ROW_W, w = i - r * ROW_W;
+    gm[(g0 + r) * ROW_W + w] = lds[r * LDS_W + w];
+  }
+}
+__device__ __forceinline__ CitMT lane_mt(uint32_t* mt, uint32_t* idx, int B, long l) {
+  CitMT r;
+  r.mt = mt + l;
+  r.idx = idx + l;
+  r.stride = B;
+  return r;
+}
+
+__global__ void k_mt_seed(uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int numpy_style) {
+  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= B) return;
+  CitMT r = lane_mt(mt, idx, B, l);
+  if (numpy_style) mt_init_genrand(r, (uint32_t)seeds[l]);
+  else mt_seed_cpython(r, seeds[l]);
+}
+
+__global__ void k_mt_draw(uint32_t* mt, uint32_t* idx, int B, int n, uint32_t* out) {
+  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= B) return;
+  CitMT r = lane_mt(mt, idx, B, l);
+  for (int i = 0; i < n; i++) out[l * n + i] = mt_next(r);
+}
+
+__global__ void k_init(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int preset) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  long g0 = (long)blockIdx.x * blockDim.x;
+  int nrows = (int)min((long)blockDim.x, (long)B - g0);
+  long l = g0 + threadIdx.x;
+  if (threadIdx.x < nrows) {
+    CitMT r = lane_mt(mt, idx, B, l);
+    mt_seed_cpython(r, seeds[l]);
+    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
+    cit_init_game(g, r, preset != 0);
+  }
+  __syncthreads();
+  stage_out(lds, games, g0, nrows);
+}
+
+__global__ void k_get_options(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, CitOpt* opts,
+                              int max_opts, int32_t* n_opts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  long g0 = (long)blockIdx.x * blockDim.x;
+  int nrows = (int)min((long)blockDim.x, (long)B - g0);
+  stage_in(lds, games, g0, nrows);
+  __syncthreads();
+  if (threadIdx.x < nrows) {
+    long l = g0 + threadIdx.x;
+    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
+    CitMT r = lane_mt(mt, idx, B, l);
+    uint64_t* sc = seer + l * CIT_SEER_MAX;
+    cit_prepare_options(g, r, sc);
+    ListSink s(opts + l * max_opts, max_opts);
+    cit_enum_options(g, s, sc);
+    g.err |= s.err;
+    n_opts[l] = s.n;
+  }
+  __syncthreads();
+  stage_out(lds, games, g0, nrows);
+}
+
+__global__ void k_carry_out(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, const CitOpt* chosen,
+                            int32_t* winner) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  long g0 = (long)blockIdx.x * blockDim.x;
+  int nrows = (int)min((long)blockDim.x, (long)B - g0);
+  stage_in(lds, games, g0, nrows);
+  __syncthreads();
+  if (threadIdx.x < nrows) {
+    long l = g0 + threadIdx.x;
+    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
+    CitMT r = lane_mt(mt, idx, B, l);
+    winner[l] = cit_carry_out(g, chosen[l], r);
+  }
+  __syncthreads();
+  stage_out(lds, games, g0, nrows);
+}
+
+__global__ void k_random_choice(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, const CitOpt* opts,
+                                int max_opts, const int32_t* n_opts, CitOpt* chosen, int32_t* k_out) {
+  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= B) return;
+  CitGame* g = reinterpret_cast<CitGame*>(games + l * ROW_W);
+  int n = n_opts[l];
+  if (n <= 0) {
+    g->err |= CIT_ERR_EMPTY;
+    k_out[l] = -1;
+    return;
+  }
+  CitMT r = lane_mt(mt, idx, B, l);
+  int k = (int)mt_randbelow(r, (uint32_t)n);
+  k_out[l] = k;
+  if (k >= max_opts) {
+    g->err |= CIT_ERR_OVERFLOW;
+    return;
+  }
+  chosen[l] = opts[l * max_opts + k];
+}
+
+// The hot loop: get_options -> randbelow -> carry_out until a winner, an error
+// or max_steps, entirely on the LDS-resident row.
+__global__ void k_rollout(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_steps,
+                          int32_t* steps_out, int32_t* winner) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  long g0 = (long)blockIdx.x * blockDim.x;
+  int nrows = (int)min((long)blockDim.x, (long)B - g0);
+  stage_in(lds, games, g0, nrows);
+  __syncthreads();
+  if (threadIdx.x < nrows) {
+    long l = g0 + threadIdx.x;
+    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
+    CitMT r = lane_mt(mt, idx, B, l);
+    uint64_t* sc = seer + l * CIT_SEER_MAX;
+    int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
+    int s = 0;
+    while (!g.terminal && !g.err && s < cap) {
+      cit_random_step(g, r, sc);
+      s++;
+    }
+    if (max_steps < 0 && s >= cap && !g.terminal && !g.err) g.err |= CIT_ERR_STEP_CAP;
+    steps_out[l] += s;
+    winner[l] = g.winner;
+  }
+  __syncthreads();
+  stage_out(lds, games, g0, nrows);
+}
+
+template <class K>
+int set_lds(K kernel, size_t bytes) {
+  return (int)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+size_t lds_bytes(int G) { return (size_t)G * LDS_W * 4; }
+
+bool g_attrs_done = false;
+int ensure_attrs() {
+  if (g_attrs_done) return 0;
+  size_t m = lds_bytes(MAX_G);
+  int e = set_lds(k_init, m);
+  if (!e) e = set_lds(k_get_options, m);
+  if (!e) e = set_lds(k_carry_out, m);
+  if (!e) e = set_lds(k_rollout, m);
+  if (!e) g_attrs_done = true;
+  return e;
+}
+
+}  // namespace
+
+#define CHECK_LAUNCH()                       \
+  do {                                       \
+    hipError_t _e = hipGetLastError();       \
+    return _e == hipSuccess ? 0 : (int)_e;   \
+  } while (0)
+
+extern "C" {
+
+int cit_abi_version(void) { return 1; }
+int cit_game_bytes(void) { return CIT_GAME_BYTES; }
+int cit_seer_scratch_words(void) { return CIT_SEER_MAX; }
+
+int cit_layout(int* out, int n) {
+  int v[] = {(int)sizeof(CitPlayer),          (int)offsetof(CitGame, deck),   (int)offsetof(CitGame, kh),
+             (int)offsetof(CitGame, roles),   (int)offsetof(CitGame, gs_state), (int)offsetof(CitGame, points),
+             (int)offsetof(CitGame, err),     (int)offsetof(CitGame, steps),  (int)sizeof(CitOpt)};
+  int k = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < k && i < n; i++) out[i] = v[i];
+  return k;
+}
+
+int cit_mt_seed(uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int numpy_style, hipStream_t stream) {
+  if (B <= 0 || !mt || !mt_idx || !seeds) return -1;
+  hipLaunchKernelGGL(k_mt_seed, dim3((B + 63) / 64), dim3(64), 0, stream, mt, mt_idx, B, seeds, numpy_style);
+  CHECK_LAUNCH();
+}
+
+int cit_mt_draw(uint32_t* mt, uint32_t* mt_idx, int B, int n, uint32_t* out, hipStream_t stream) {
+  if (B <= 0 || n < 0 || !mt || !mt_idx || !out) return -1;
+  hipLaunchKernelGGL(k_mt_draw, dim3((B + 63) / 64), dim3(64), 0, stream, mt, mt_idx, B, n, out);
+  CHECK_LAUNCH();
+}
+
+int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int preset,
+             hipStream_t stream) {
+  if (B <= 0 || !games || !mt || !mt_idx || !seeds) return -1;
+  if (int e = ensure_attrs()) return e;
+  const int G = 64;
+  hipLaunchKernelGGL(k_init, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx, B,
+                     seeds, preset);
+  CHECK_LAUNCH();
+}
+
+int cit_get_options(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, CitOption* opts,
+                    int max_opts, int32_t* n_opts, hipStream_t stream) {
+  if (B <= 0 || max_opts < 0 || !games || !mt || !mt_idx || !seer || !n_opts || (max_opts && !opts)) return -1;
+  if (int e = ensure_attrs()) return e;
+  const int G = 64;
+  hipLaunchKernelGGL(k_get_options, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+                     mt_idx, seer, B, (CitOpt*)opts, max_opts, n_opts);
+  CHECK_LAUNCH();
+}
+
+int cit_random_choice(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitOption* opts, int max_opts,
+                      const int32_t* n_opts, CitOption* chosen, int32_t* k_out, hipStream_t stream) {
+  if (B <= 0 || max_opts < 0 || !games || !mt || !mt_idx || !n_opts || !chosen || !k_out || (max_opts && !opts))
+    return -1;
+  hipLaunchKernelGGL(k_random_choice, dim3((B + 63) / 64), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, B,
+                     (const CitOpt*)opts, max_opts, n_opts, (CitOpt*)chosen, k_out);
+  CHECK_LAUNCH();
+}
+
+int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitOption* chosen, int32_t* winner,
+                  hipStream_t stream) {
+  if (B <= 0 || !games || !mt || !mt_idx || !chosen || !winner) return -1;
+  if (int e = ensure_attrs()) return e;
+  const int G = 64;
+  hipLaunchKernelGGL(k_carry_out, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+                     mt_idx, B, (const CitOpt*)chosen, winner);
+  CHECK_LAUNCH();
+}
+
+int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
+                       int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream) {
+  if (B <= 0 || !games || !mt || !mt_idx || !seer || !steps || !winner) return -1;
+  int G = games_per_block <= 0 ? 16 : games_per_block;
+  if (G > MAX_G) return -1;
+  if (int e = ensure_attrs()) return e;
+  hipLaunchKernelGGL(k_rollout, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx,
+                     seer, B, max_steps, steps, winner);
+  CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -96,7 +96,8 @@ void cith_rollout(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B
   for (int l = 0; l < B; l++) {
     CitMT r = lane_rng(mt, idx, B, l);
     int s = 0;
-    while (!g[l].terminal && !g[l].err && (max_steps < 0 || s < max_steps)) {
+    int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
+    while (!g[l].terminal && !g[l].err && s < cap) {
       cit_random_step(g[l], r, seer + (long)l * CIT_SEER_MAX);
       s++;
     }

@@ -18,7 +18,7 @@ ROLE_BEWITCHED, ROLE_NONE = 27, 255
 
 ERR_BITS = {
     0x1: "OverflowError", 0x2: "IndexError", 0x4: "KeyError", 0x8: "ValueError",
-    0x10: "IndexError", 0x20: "AttributeError", 0x40: "NotImplementedError", 0x80: "TypeError",
+    0x10: "IndexError", 0x20: "AttributeError", 0x40: "NotImplementedError", 0x80: "TypeError", 0x100: "StepCap",
 }
 
 

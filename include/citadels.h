@@ -1,0 +1,103 @@
+/* citadels.h — C ABI of libcitadels_hip.so, the MI355X (gfx950) Citadels
+ * rules engine.  Plain pointers and sizes only; every buffer argument is a
+ * DEVICE pointer (hipMalloc / torch CUDA tensor storage) and every call is
+ * asynchronous on `stream`.  Return value: 0, or a hipError_t / -1 (bad args).
+ *
+ * The reference (davpat108/CITADELS_self_play) has no FFI: its hot path is a
+ * Python object API.  Each entry point below replaces one of its calls, cited
+ * file:line; the Python binding a maintainer would add is in INTEGRATION.md.
+ *
+ * Data (see citadels_self_play_amd/csrc/cit_core.h for the exact layout):
+ *   games  : B rows of cit_game_bytes() bytes, one packed game per row.
+ *   mt     : uint32 [624][B] CPython MT19937 words, structure-of-arrays.
+ *   mt_idx : uint32 [B] stream positions.  Lane l reproduces the reference run
+ *            after `random.seed(seeds[l])`.
+ *   seer   : uint64 [B][cit_seer_scratch_words()] scratch for the Seer's
+ *            RNG-drawn give-back permutations (state 8).
+ *   opts   : CitOption [B][max_opts] (16 B each, layout below).
+ */
+#ifndef CITADELS_H
+#define CITADELS_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* 16-byte option descriptor.  name = option id in the order of
+ * game/option.py:34-45; perp = perpetrator; target = player or -1.
+ * Per name: role_pick a=rank | gold_or_card a=0 gold,1 card |
+ * which_card_to_keep a,b=cards (b=255: single) | blackmail_response a=0 pay,1 not |
+ * reveal_* a=0 reveal,1 not | build a=card c=replica | empty_option a=0 fresh
+ * GameState(5,perp), 1 the game's next_gamestate | finish_round flags bit0
+ * next_witch bit1 crown | laboratory/lighthouse/museum/weapon_storage/warlord/
+ * marshal a=card | magic_school a=suit | assassination/bewitching/steal a=rank |
+ * magistrate_warrant a=real b,c=fakes | blackmail a=real b=fake | spy a=suit |
+ * discard_and_draw x=hand-slot mask | take_from_hand a=card flags bit0 build
+ * c=replica | give_back_card b=count, x=cards (byte i) | give_crown a=0 card,1
+ * gold,2 nothing | cardinal_exchange a=card b=#given c=replica flags bit0
+ * factory x=hand-slot mask | abbot_gold_or_card a=#religious b=#card |
+ * navigator_gold_card a=0 4gold,1 4card | scholar_card_pick a=card |
+ * diplomat_exchange a=choice b=give c=money_owed. */
+typedef struct CitOption {
+  uint8_t name, perp;
+  int8_t target;
+  uint8_t a, b, c, d, flags;
+  uint64_t x;
+} CitOption;
+
+int cit_abi_version(void);
+int cit_game_bytes(void);              /* row width of `games` */
+int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
+int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
+
+/* random.seed(seeds[l]) (CPython init_by_array) or, numpy_style != 0,
+ * np.random.seed(seeds[l]) (init_genrand) for every lane. */
+int cit_mt_seed(uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int numpy_style,
+                hipStream_t stream);
+/* n raw 32-bit outputs of every lane's stream into out[B][n] (RNG parity tests). */
+int cit_mt_draw(uint32_t* mt, uint32_t* mt_idx, int B, int n, uint32_t* out, hipStream_t stream);
+
+/* Game(preset) + create_game's setup_round for every lane, with the lane's
+ * stream freshly seeded from seeds[l]: replaces `random.seed(s); create_game()`
+ * (run_utils.py:20-27, game/game.py:17-24,420-540,144-171).  preset=0 builds
+ * the random-role Game() (game.py:491-520). */
+int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int preset,
+             hipStream_t stream);
+
+/* Game.get_options_from_state() for every lane (game/game.py:415-418 ->
+ * game/agent.py:50-83): writes the ordered option list to opts[l][0..) and its
+ * length to n_opts[l] (n_opts may exceed max_opts; the list is then cut).
+ * Mutates the game and consumes its stream exactly where the reference does
+ * (scholar state 9, seer state 8). */
+int cit_get_options(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, CitOption* opts,
+                    int max_opts, int32_t* n_opts, hipStream_t stream);
+
+/* random.choice(options) for every lane (compare_to_random.py:38,
+ * run_utils.py:39; Lib/random.py:371-373): k = _randbelow(n_opts[l]) drawn
+ * from the lane's stream, chosen[l] = opts[l][k], k_out[l] = k.  An empty
+ * list sets the lane's IndexError bit and k_out = -1 (the reference raises). */
+int cit_random_choice(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitOption* opts, int max_opts,
+                      const int32_t* n_opts, CitOption* chosen, int32_t* k_out, hipStream_t stream);
+
+/* option.carry_out(game) for every lane (game/option.py:118-122 ->
+ * game/option_functions.py): chosen[l] must come from the lane's last
+ * cit_get_options.  winner[l] = index of the returned winning Agent, or -1
+ * for None/False. */
+int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitOption* chosen,
+                  int32_t* winner, hipStream_t stream);
+
+/* The fused random-policy step loop of compare_to_random.py:37-39 /
+ * run_utils.py:37-41 (get_options -> random.choice -> carry_out) for up to
+ * max_steps steps per lane (max_steps < 0: until a winner or an error).
+ * steps[l] += steps taken; winner[l] as above.  games_per_block (1..64, 0 =
+ * default) sets how many lanes share a workgroup's LDS. */
+int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
+                       int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,41 @@
+"""CPU-side checks of the C ABI: the shared library loads here (no GPU
+needed to load it), exports every symbol include/citadels.h declares, and its
+struct layout matches the Python mirror.  No compute calls."""
+import ctypes as C
+import os
+
+import pytest
+
+from citadels_self_play_amd import _lib
+from citadels_self_play_amd import layout as L
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build_hip()
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    names = _lib.declared_symbols()
+    assert len(names) >= 9
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _lib._SIGS, n
+
+
+def test_layout_matches(lib):
+    out = (C.c_int * 16)()
+    n = lib.cit_layout(out, 16)
+    assert list(out[:n]) == L.expected_layout()
+    assert lib.cit_game_bytes() == L.GAME_BYTES
+    assert lib.cit_seer_scratch_words() == L.SEER_MAX
+    assert lib.cit_abi_version() == 1
+
+
+def test_bad_args_rejected(lib):
+    # argument validation happens before any launch: no GPU is touched
+    assert lib.cit_rollout_random(None, None, None, None, 0, -1, 0, None, None, None) == -1
+    assert lib.cit_init(None, None, None, 4, None, 1, None) == -1

@@ -49,6 +49,11 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise NativeError("libcitadels_hip.so is not built (run __graft_entry__.build()); "
                           "the Citadels engine has no CPU fallback")
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7, and
+    # the library's NEEDED entry resolves to whichever copy is already loaded
+    # (same SONAME).  Importing torch first makes that torch's copy, so device
+    # pointers and streams from torch are valid in our launches.
+    import torch  # noqa: F401
     lib = C.CDLL(LIB_PATH)
     for name, (args, res) in _SIGS.items():
         fn = getattr(lib, name)

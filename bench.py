@@ -80,7 +80,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="games per GPU")
-    ap.add_argument("--games-per-block", type=int, default=16)
+    ap.add_argument("--games-per-block", type=int, default=0, help="0 = auto (1 game per wavefront at B=4096)")
     ap.add_argument("--cpu-procs", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

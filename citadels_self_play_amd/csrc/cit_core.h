@@ -180,29 +180,30 @@ static_assert(CIT_GAME_BYTES % 16 == 0, "row must be 16-byte aligned");
 
 // ----------------------------------------------------------------- MT19937
 // Per-lane MT19937 laid out structure-of-arrays: word i of lane l at
-// mt[i*stride + l]; idx[l] is the position (624 = twist next).
+// mt[i*stride + l].  The stream position lives in a register while a kernel
+// runs (`pos`); callers load it from / store it to the mt_idx array.
 #define CIT_MT_N 624
 struct CitMT {
   uint32_t* mt;
-  uint32_t* idx;
   int stride;
+  uint32_t pos;   // 624 = twist next
 };
 
 CIT_HD uint32_t mt_word(const CitMT& r, int i) { return r.mt[(long)i * r.stride]; }
 CIT_HD void mt_set(const CitMT& r, int i, uint32_t v) { r.mt[(long)i * r.stride] = v; }
 
 // init_genrand (numpy legacy `RandomState.seed(int)`)
-CIT_HDI void mt_init_genrand(const CitMT& r, uint32_t s) {
+CIT_HDI void mt_init_genrand(CitMT& r, uint32_t s) {
   mt_set(r, 0, s);
   for (int i = 1; i < CIT_MT_N; i++) {
     s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i;
     mt_set(r, i, s);
   }
-  *r.idx = CIT_MT_N;
+  r.pos = CIT_MT_N;
 }
 
 // CPython random.seed(int): init_by_array(key = 32-bit little-endian words of |seed|)
-CIT_HDI void mt_seed_cpython(const CitMT& r, uint64_t seed) {
+CIT_HDI void mt_seed_cpython(CitMT& r, uint64_t seed) {
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   int klen = (seed >> 32) ? 2 : 1;
   mt_init_genrand(r, 19650218u);
@@ -225,7 +226,7 @@ CIT_HDI void mt_seed_cpython(const CitMT& r, uint64_t seed) {
     if (i >= CIT_MT_N) { mt_set(r, 0, v); i = 1; }
   }
   mt_set(r, 0, 0x80000000u);
-  *r.idx = CIT_MT_N;
+  r.pos = CIT_MT_N;
 }
 
 CIT_HDI void mt_twist(const CitMT& r) {
@@ -242,14 +243,14 @@ CIT_HDI void mt_twist(const CitMT& r) {
   }
 }
 
-CIT_HD uint32_t mt_next(const CitMT& r) {
-  uint32_t i = *r.idx;
+CIT_HD uint32_t mt_next(CitMT& r) {
+  uint32_t i = r.pos;
   if (i >= CIT_MT_N) {
     mt_twist(r);
     i = 0;
   }
   uint32_t y = mt_word(r, (int)i);
-  *r.idx = i + 1;
+  r.pos = i + 1;
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680u;
   y ^= (y << 15) & 0xefc60000u;
@@ -264,7 +265,7 @@ CIT_HD int bit_length(uint32_t n) {
 }
 
 // random._randbelow_with_getrandbits (Lib/random.py:239-249)
-CIT_HD uint32_t mt_randbelow(const CitMT& r, uint32_t n) {
+CIT_HD uint32_t mt_randbelow(CitMT& r, uint32_t n) {
   if (!n) return 0;
   int k = bit_length(n);
   uint32_t v = mt_next(r) >> (32 - k);
@@ -273,7 +274,7 @@ CIT_HD uint32_t mt_randbelow(const CitMT& r, uint32_t n) {
 }
 
 // random.random() / numpy random_sample(): 53-bit double from two draws
-CIT_HD double mt_random(const CitMT& r) {
+CIT_HD double mt_random(CitMT& r) {
   uint32_t a = mt_next(r) >> 5, b = mt_next(r) >> 6;
   return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
 }

@@ -59,6 +59,13 @@ CIT_HD int pop_front(uint8_t* a, uint8_t& n) {
 #define JD(p) (p).jd, (p).n_jd, CIT_JD_CAP
 #define MUSEUM(p) (p).museum, (p).n_museum, CIT_MUSEUM_CAP
 CIT_HD bool p_has(const CitPlayer& p, int t) { return has_type(p.build, p.n_build, t); }
+// bit t set iff a card of type t is in the list
+CIT_HD uint64_t type_mask(const uint8_t* a, int n) {
+  uint64_t m = 0;
+  for (int i = 0; i < n; i++) m |= 1ull << card_type(a[i]);
+  return m;
+}
+#define HAS(mask, t) (((mask) >> (t)) & 1)
 
 // ------------------------------------------------------------ deck (ring)
 CIT_HD int deck_at(const CitGame& g, int i) { return g.deck[(g.deck_head + i) & (CIT_DECK_CAP - 1)]; }
@@ -90,7 +97,7 @@ CIT_HD int deck_take_like(CitGame& g, int c) {
 }
 // random.shuffle (Lib/random.py:380-392) over any indexable sequence
 template <class At>
-CIT_HD void shuffle_seq(const CitMT& rng, int n, At at) {
+CIT_HD void shuffle_seq(CitMT& rng, int n, At at) {
   for (int i = n - 1; i > 0; i--) {
     int j = (int)mt_randbelow(rng, (uint32_t)(i + 1));
     uint8_t t = at(i);
@@ -98,14 +105,14 @@ CIT_HD void shuffle_seq(const CitMT& rng, int n, At at) {
     at(j) = t;
   }
 }
-CIT_HD void shuffle_arr(const CitMT& rng, uint8_t* a, int n) {
+CIT_HD void shuffle_arr(CitMT& rng, uint8_t* a, int n) {
   shuffle_seq(rng, n, [a](int i) -> uint8_t& { return a[i]; });
 }
-CIT_HD void deck_shuffle(CitGame& g, const CitMT& rng) {
+CIT_HD void deck_shuffle(CitGame& g, CitMT& rng) {
   shuffle_seq(rng, g.n_deck, [&g](int i) -> uint8_t& { return deck_ref(g, i); });
 }
 // reshuffle_deck_if_empty (option_functions.py:564-570)
-CIT_HD void reshuffle_if_empty(CitGame& g, const CitMT& rng) {
+CIT_HD void reshuffle_if_empty(CitGame& g, CitMT& rng) {
   if (g.n_deck || !g.n_discard) return;
   shuffle_arr(rng, g.discard, g.n_discard);
   g.deck_head = 0;
@@ -113,7 +120,7 @@ CIT_HD void reshuffle_if_empty(CitGame& g, const CitMT& rng) {
   g.n_deck = g.n_discard;
   g.n_discard = 0;
 }
-CIT_HD void draw_into(CitGame& g, const CitMT& rng, uint8_t* a, uint8_t& n, int cap, int k) {
+CIT_HD void draw_into(CitGame& g, CitMT& rng, uint8_t* a, uint8_t& n, int cap, int k) {
   for (int i = 0; i < k; i++) {
     reshuffle_if_empty(g, rng);
     put_card(g, a, n, cap, deck_draw(g));
@@ -281,7 +288,7 @@ CIT_HD void setup_next_player(CitGame& g, int current) {
   }
 }
 
-CIT_HD void cit_setup_round(CitGame& g, const CitMT& rng) {
+CIT_HD void cit_setup_round(CitGame& g, CitMT& rng) {
   for (int r = 0; r < 8; r++) g.rp[r] = 0;
   g.n_used_roles = 0;
   uint8_t pool[8];
@@ -305,7 +312,7 @@ CIT_HD void cit_setup_round(CitGame& g, const CitMT& rng) {
 
 // Game(preset) + set_initial_variables + create_game's setup_round, for a
 // game whose CPython stream has just been seeded.
-CIT_HD void cit_init_game(CitGame& g, const CitMT& rng, bool preset) {
+CIT_HD void cit_init_game(CitGame& g, CitMT& rng, bool preset) {
   uint8_t* z = (uint8_t*)&g;
   for (int i = 0; i < (int)sizeof(CitGame); i++) z[i] = 0;
   // building_cards multiplicities per type 0..15, one nibble each (config.py:2-52)
@@ -423,25 +430,22 @@ CIT_HD CitOpt mk(int name, int perp, int target = -1, int a = 0, int b = 0, int 
 enum { OF_TUPLE = 1, OF_NEXT_WITCH = 1, OF_CROWN = 2, OF_BUILD = 1, OF_FACTORY = 1 };
 
 // Sinks: emit() returns true to stop the enumeration.
-struct CountSink {
-  int n = 0;
-  uint32_t err = 0;
-  CIT_HD bool emit(const CitOpt&) { n++; return false; }
-  template <class F> CIT_HD bool block(int cnt, F&&) { n += cnt; return false; }
-};
+// PickSink(k) stops at the k-th option (out); PickSink(-1) just counts (n).
+// The fused rollout uses this one sink for both passes, so the enumerator is
+// instantiated once in that kernel.
 struct PickSink {
   int k;
+  int n = 0;
   CitOpt out;
   uint32_t err = 0;
   CIT_HD explicit PickSink(int kk) : k(kk) { out = mk(O_NUM_NAMES, 0); }
   CIT_HD bool emit(const CitOpt& o) {
-    if (k == 0) { out = o; return true; }
-    k--;
+    if (n++ == k) { out = o; return true; }
     return false;
   }
   template <class F> CIT_HD bool block(int cnt, F&& f) {
-    if (k < cnt) { out = f(k); return true; }
-    k -= cnt;
+    if (k >= n && k < n + cnt) { out = f(k - n); n = k + 1; return true; }
+    n += cnt;
     return false;
   }
 };
@@ -504,17 +508,17 @@ CIT_HD uint64_t unrank_comb(int n, int k, long idx) {
 // ================================================== option generators
 // build_options / get_builds (agent_functions.py:108-130)
 template <class S>
-CIT_HD bool gen_builds(const CitGame& g, int a, S& s) {
+CIT_HD bool gen_builds(const CitGame& g, int a, uint64_t bm, S& s) {
   const CitPlayer& P = g.pl[a];
   int lim = P.role == R_ARCHITECT ? 3 : P.role == R_SCHOLAR ? 2 : (P.role == R_BISHOP || P.role == R_NAVIGATOR) ? 0 : 1;
   int done = g.gs_adm[ADM_NON_TRADE] + (P.role == R_TRADER ? 0 : g.gs_adm[ADM_TRADE]);
   if (done >= lim) return false;
-  bool factory = p_has(P, 35);
+  bool factory = HAS(bm, 35);
   uint64_t seen = 0;
   for (int i = 0; i < P.n_hand; i++) {
     int c = P.hand[i], t = card_type(c);
     int cost = card_cost(c) + (factory && card_suit(c) == SUIT_UNIQUE ? 1 : 0);
-    int rep = (p_has(P, t) && !P.replicas) ? P.replicas + 1 : 0;
+    int rep = (HAS(bm, t) && !P.replicas) ? P.replicas + 1 : 0;
     if (cost <= P.gold && !((seen >> t) & 1)) {
       seen |= 1ull << t;
       EMIT(mk(O_BUILD, a, -1, c, 0, rep));
@@ -715,22 +719,23 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
 template <class S>
 CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
   const CitPlayer& P = g.pl[a];
-  if (gen_builds(g, a, s)) return true;
+  const uint64_t bm = type_mask(P.build, P.n_build);
+  if (gen_builds(g, a, bm, s)) return true;
   if (!g.gs_adm[ADM_ABILITY])
     if (gen_role(g, a, s)) return true;
   if (P.role == R_ABBOT && !g.gs_adm[ADM_BEGGED]) EMIT(mk(O_ABBOT_BEG, a));
   if ((P.role == R_WARLORD || P.role == R_MARSHAL || P.role == R_DIPLOMAT) && !g.gs_adm[ADM_TAKE_GOLD])
     EMIT(mk(O_TAKE_GOLD_WAR, a));
-  if (p_has(P, 21) && P.gold >= 2 && !g.gs_adm[ADM_SMITHY]) EMIT(mk(O_SMITHY, a));
-  if (p_has(P, 22) && !g.gs_adm[ADM_LAB])
+  if (HAS(bm, 21) && P.gold >= 2 && !g.gs_adm[ADM_SMITHY]) EMIT(mk(O_SMITHY, a));
+  if (HAS(bm, 22) && !g.gs_adm[ADM_LAB])
     for (int i = 0; i < P.n_hand; i++) EMIT(mk(O_LAB, a, -1, P.hand[i]));
-  if (!g.gs_adm[ADM_MAGIC_SCHOOL] && p_has(P, 25))
+  if (!g.gs_adm[ADM_MAGIC_SCHOOL] && HAS(bm, 25))
     for (int su = 0; su < 5; su++) EMIT(mk(O_MAGIC_SCHOOL, a, -1, su));
-  if (p_has(P, 27))
+  if (HAS(bm, 27))
     for (int p = 0; p < CIT_NP; p++)
       if (p != a)
         for (int i = 0; i < g.pl[p].n_build; i++) EMIT(mk(O_WEAPON_STORAGE, a, p, g.pl[p].build[i]));
-  if (p_has(P, 29) && (P.flags & PF_LIGHTHOUSE)) {
+  if (HAS(bm, 29) && (P.flags & PF_LIGHTHOUSE)) {
     uint64_t seen = 0;
     for (int i = 0; i < g.n_deck; i++) {
       int c = deck_at(g, i), t = card_type(c);
@@ -740,7 +745,7 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
       }
     }
   }
-  if (p_has(P, 34) && !g.gs_adm[ADM_MUSEUM]) {
+  if (HAS(bm, 34) && !g.gs_adm[ADM_MUSEUM]) {
     uint64_t seen = 0;
     for (int i = 0; i < P.n_hand; i++) {
       int c = P.hand[i], t = card_type(c);
@@ -766,7 +771,8 @@ CIT_HD bool gen_wizard_take(const CitGame& g, int a, S& s) {
   }
   if (e < 0) { s.err |= CIT_ERR_ATTR; return true; }
   int tgt = g.kh[e].target;
-  bool factory = p_has(P, 35);
+  const uint64_t bm = type_mask(P.build, P.n_build);
+  bool factory = HAS(bm, 35);
   int rep = 0;
   uint64_t seen_take = 0, seen_b0 = 0, seen_b1 = 0;
   int emitted = 0;
@@ -778,7 +784,7 @@ CIT_HD bool gen_wizard_take(const CitGame& g, int a, S& s) {
       EMIT(mk(O_TAKE_FROM_HAND, a, tgt, c, 0, 0, 0));
     }
     int cost = card_cost(c) + (factory && card_suit(c) == SUIT_UNIQUE ? 1 : 0);
-    if (p_has(P, t)) rep = P.replicas + 1;
+    if (HAS(bm, t)) rep = P.replicas + 1;
     uint64_t& seen = rep == 0 ? seen_b0 : seen_b1;   // rep takes at most one non-zero value
     if (cost <= P.gold && !((seen >> t) & 1)) {
       seen |= 1ull << t;
@@ -897,7 +903,7 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
 //    permutations go to `seer` (CIT_SEER_MAX packed options per lane:
 //    card i in byte i, handout count in byte 7).
 #define CIT_SEER_MAX (5 * CIT_HAND_CAP * 3)
-CIT_HD void cit_prepare_options(CitGame& g, const CitMT& rng, uint64_t* seer) {
+CIT_HD void cit_prepare_options(CitGame& g, CitMT& rng, uint64_t* seer) {
   g.n_sch = 0;
   if ((g.gs_state != 9 && g.gs_state != 8) || g.gs_pid < 0) return;
   const CitPlayer& P = g.pl[g.gs_pid];
@@ -945,7 +951,7 @@ CIT_HD void cit_prepare_options(CitGame& g, const CitMT& rng, uint64_t* seer) {
 }
 
 CIT_HD int cit_count_options(const CitGame& g, uint32_t& err, const uint64_t* seer) {
-  CountSink s;
+  PickSink s(-1);
   cit_enum_options(g, s, seer);
   err |= s.err;
   return s.n;
@@ -1011,7 +1017,7 @@ CIT_HD void settle(CitGame& g, int name, int a, int t, int card) {
 }
 
 // finish_main_sequnce_actions (option_functions.py:189-243); returns winner or -1
-CIT_HD int do_finish(CitGame& g, const CitOpt& o, const CitMT& rng) {
+CIT_HD int do_finish(CitGame& g, const CitOpt& o, CitMT& rng) {
   int a = o.perp;
   CitPlayer& P = g.pl[a];
   bool dead = rp_of(g, P.role) & RP_DEAD;
@@ -1052,7 +1058,7 @@ CIT_HD int do_finish(CitGame& g, const CitOpt& o, const CitMT& rng) {
 
 // option.carry_out (option.py:118-122): transition then is_last_round.
 // Returns the winner's index, or -1.
-CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, const CitMT& rng) {
+CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
   int a = o.perp;
   CitPlayer& P = g.pl[a];
   int w = -1;
@@ -1441,7 +1447,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, const CitMT& rng) {
 
 // One random-policy step (compare_to_random.py:37-39): get_options ->
 // random.choice -> carry_out.  Returns 1 when the lane is done (winner or error).
-CIT_HD int cit_random_step(CitGame& g, const CitMT& rng, uint64_t* seer) {
+CIT_HD int cit_random_step(CitGame& g, CitMT& rng, uint64_t* seer) {
   cit_prepare_options(g, rng, seer);
   uint32_t err = 0;
   int n = cit_count_options(g, err, seer);

@@ -31,11 +31,11 @@ __device__ __forceinline__ void stage_out(const uint32_t* lds, uint32_t* __restr
     gm[(g0 + r) * ROW_W + w] = lds[r * LDS_W + w];
   }
 }
-__device__ __forceinline__ CitMT lane_mt(uint32_t* mt, uint32_t* idx, int B, long l) {
+__device__ __forceinline__ CitMT lane_mt(uint32_t* mt, const uint32_t* idx, int B, long l) {
   CitMT r;
   r.mt = mt + l;
-  r.idx = idx + l;
   r.stride = B;
+  r.pos = idx[l];
   return r;
 }
 
@@ -45,6 +45,7 @@ __global__ void k_mt_seed(uint32_t* mt, uint32_t* idx, int B, const uint64_t* se
   CitMT r = lane_mt(mt, idx, B, l);
   if (numpy_style) mt_init_genrand(r, (uint32_t)seeds[l]);
   else mt_seed_cpython(r, seeds[l]);
+  idx[l] = r.pos;
 }
 
 __global__ void k_mt_draw(uint32_t* mt, uint32_t* idx, int B, int n, uint32_t* out) {
@@ -52,6 +53,7 @@ __global__ void k_mt_draw(uint32_t* mt, uint32_t* idx, int B, int n, uint32_t* o
   if (l >= B) return;
   CitMT r = lane_mt(mt, idx, B, l);
   for (int i = 0; i < n; i++) out[l * n + i] = mt_next(r);
+  idx[l] = r.pos;
 }
 
 __global__ void k_init(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int preset) {
@@ -64,6 +66,7 @@ __global__ void k_init(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, cons
     mt_seed_cpython(r, seeds[l]);
     CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
     cit_init_game(g, r, preset != 0);
+    idx[l] = r.pos;
   }
   __syncthreads();
   stage_out(lds, games, g0, nrows);
@@ -86,6 +89,7 @@ __global__ void k_get_options(uint32_t* games, uint32_t* mt, uint32_t* idx, uint
     cit_enum_options(g, s, sc);
     g.err |= s.err;
     n_opts[l] = s.n;
+    idx[l] = r.pos;
   }
   __syncthreads();
   stage_out(lds, games, g0, nrows);
@@ -103,6 +107,7 @@ __global__ void k_carry_out(uint32_t* games, uint32_t* mt, uint32_t* idx, int B,
     CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
     CitMT r = lane_mt(mt, idx, B, l);
     winner[l] = cit_carry_out(g, chosen[l], r);
+    idx[l] = r.pos;
   }
   __syncthreads();
   stage_out(lds, games, g0, nrows);
@@ -121,6 +126,7 @@ __global__ void k_random_choice(uint32_t* games, uint32_t* mt, uint32_t* idx, in
   }
   CitMT r = lane_mt(mt, idx, B, l);
   int k = (int)mt_randbelow(r, (uint32_t)n);
+  idx[l] = r.pos;
   k_out[l] = k;
   if (k >= max_opts) {
     g->err |= CIT_ERR_OVERFLOW;
@@ -152,6 +158,7 @@ __global__ void k_rollout(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t
     if (max_steps < 0 && s >= cap && !g.terminal && !g.err) g.err |= CIT_ERR_STEP_CAP;
     steps_out[l] += s;
     winner[l] = g.winner;
+    idx[l] = r.pos;
   }
   __syncthreads();
   stage_out(lds, games, g0, nrows);
@@ -252,7 +259,10 @@ int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitO
 int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
                        int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream) {
   if (B <= 0 || !games || !mt || !mt_idx || !seer || !steps || !winner) return -1;
-  int G = games_per_block <= 0 ? 16 : games_per_block;
+  // 0 = auto: one game per wavefront until the chip has ~4 waves per SIMD
+  // (B = 4096), then more lanes per wave (divergence costs less than idle SIMDs)
+  int G = games_per_block > 0 ? games_per_block : (B >= 8192 ? B / 4096 : 1);
+  if (G > 16 && games_per_block <= 0) G = 16;
   if (G > MAX_G) return -1;
   if (int e = ensure_attrs()) return e;
   hipLaunchKernelGGL(k_rollout, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx,

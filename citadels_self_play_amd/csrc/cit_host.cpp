@@ -35,32 +35,40 @@ int cith_layout(int* out, int n) {
 static CitMT lane_rng(uint32_t* mt, uint32_t* idx, int B, int l) {
   CitMT r;
   r.mt = mt + l;
-  r.idx = idx + l;
   r.stride = B;
+  r.pos = idx[l];
   return r;
 }
+#define SAVE(r) idx[l] = (r).pos
 
 void cith_mt_seed(uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int numpy_style) {
   for (int l = 0; l < B; l++) {
     CitMT r = lane_rng(mt, idx, B, l);
     if (numpy_style) mt_init_genrand(r, (uint32_t)seeds[l]);
     else mt_seed_cpython(r, seeds[l]);
+    SAVE(r);
   }
 }
 
 void cith_mt_draw(uint32_t* mt, uint32_t* idx, int B, int lane, int n, uint32_t* out) {
-  CitMT r = lane_rng(mt, idx, B, lane);
+  int l = lane;
+  CitMT r = lane_rng(mt, idx, B, l);
   for (int i = 0; i < n; i++) out[i] = mt_next(r);
+  SAVE(r);
 }
 
 void cith_mt_randbelow(uint32_t* mt, uint32_t* idx, int B, int lane, uint32_t bound, int n, uint32_t* out) {
-  CitMT r = lane_rng(mt, idx, B, lane);
+  int l = lane;
+  CitMT r = lane_rng(mt, idx, B, l);
   for (int i = 0; i < n; i++) out[i] = mt_randbelow(r, bound);
+  SAVE(r);
 }
 
 void cith_mt_random(uint32_t* mt, uint32_t* idx, int B, int lane, int n, double* out) {
-  CitMT r = lane_rng(mt, idx, B, lane);
+  int l = lane;
+  CitMT r = lane_rng(mt, idx, B, l);
   for (int i = 0; i < n; i++) out[i] = mt_random(r);
+  SAVE(r);
 }
 
 void cith_init(CitGame* g, uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int preset) {
@@ -68,6 +76,7 @@ void cith_init(CitGame* g, uint32_t* mt, uint32_t* idx, int B, const uint64_t* s
     CitMT r = lane_rng(mt, idx, B, l);
     mt_seed_cpython(r, seeds[l]);
     cit_init_game(g[l], r, preset != 0);
+    SAVE(r);
   }
 }
 
@@ -81,6 +90,7 @@ void cith_get_options(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, i
     cit_enum_options(g[l], s, sc);
     g[l].err |= s.err;
     n_opts[l] = s.n;
+    SAVE(r);
   }
 }
 
@@ -88,6 +98,7 @@ void cith_carry_out(CitGame* g, uint32_t* mt, uint32_t* idx, int B, const CitOpt
   for (int l = 0; l < B; l++) {
     CitMT r = lane_rng(mt, idx, B, l);
     winner[l] = cit_carry_out(g[l], chosen[l], r);
+    SAVE(r);
   }
 }
 
@@ -103,6 +114,7 @@ void cith_rollout(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B
     }
     steps[l] = s;
     winner[l] = g[l].winner;
+    SAVE(r);
   }
 }
 

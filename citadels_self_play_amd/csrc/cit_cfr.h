@@ -1,0 +1,548 @@
+// MCCFR search on packed rows (algorithms/deep_mccfr.py), host+device.
+//
+// One tree per workgroup on the device.  The tree lives in HBM as a node
+// pool: CfrNode headers, CfrEdge records (option + child + regret/strategy
+// rows) and one packed game row per node (the reference's `deepcopy(game)`
+// becomes a 1456-byte row copy done by the whole 64-lane team).  Every lane
+// of the team runs the same scalar search code on the same data (uniform
+// control flow, identical writes), so row copies and other data-parallel
+// pieces can be split across lanes without divergence.
+//
+//   CfrNode / cfr_node       CFRNode.__init__ + skip_false_choice   deep_mccfr.py:8-49
+//   cfr_update_strategy      update_strategy                        :292-319
+//   cfr_choose / cfr_live    action_choice, weighted_average_...   :51-91, game.py:312-317
+//   cfr_expand_*             expand / expand_role_pick / _for_original_player / _for_opponents  :93-179
+//   cfr_backprop             backpropagate + update_regrets          :231-256, 276-290
+//   cfr_train                cfr_train                               :187-205
+// fp64 follows numpy's operation order: np.sum = pairwise (8 accumulators,
+// blocks of <= 128), axis-0 sums and cumsum sequential, choice(p) = kahan
+// check + cumsum + cdf/cdf[-1] + searchsorted(right) on a 53-bit double.
+// np.exp is the only op not restated bit for bit (libm/ocml exp; both within
+// 1 ulp of numpy's SIMD exp): strategies agree to ~1e-15 relative.
+#pragma once
+#include <math.h>
+
+#include "cit_engine.h"
+
+#define CFR_OPP_CHILDREN 10
+#define CFR_ROLE_CHILDREN 10
+#define CFR_OPT_CAP 512
+#define CFR_LN13 0x1.0ca937be1b9dcp-2   // np.log(1.3)
+#define CFR_ATOL 1.4901161193847656e-08  // sqrt(finfo(float64).eps), numpy choice's p check
+
+enum { NF_ROLE_PICK = 1, NF_TERMINAL = 2, NF_PRED = 4 };
+
+struct CfrNode {                       // 168 B
+  int32_t parent, first_edge;
+  int16_t n_children, edge_cap, depth;
+  int8_t player, gs_state;
+  uint8_t flags;
+  int8_t winner;
+  uint8_t pad[6];
+  double nv[6], wp[6], pred[6];
+};
+struct CfrEdge {                       // 168 B; normal nodes use index 0 of R/S/CS
+  CitOpt opt;
+  int32_t child, pad;
+  double R[6], S[6], CS[6];
+};
+static_assert(sizeof(CfrNode) == 168, "CfrNode layout");
+static_assert(sizeof(CfrEdge) == 168, "CfrEdge layout");
+
+struct CfrTree {
+  CfrNode* nodes;
+  CfrEdge* edges;
+  uint32_t* rows;                      // node_cap rows of CIT_GAME_BYTES
+  int node_cap, edge_cap;
+  int n_nodes, n_edges;
+  int orig;
+  bool training;
+  CitMT py;                            // the games' CPython stream
+  CitMT np;                            // numpy's global RandomState
+  uint64_t* seer;
+  CitOpt* optbuf;                      // CFR_OPT_CAP descriptors
+  CitGame* w0;                         // working rows (LDS on the device)
+  CitGame* w1;
+  uint8_t* tmp;                        // >= CIT_USED_CAP bytes scratch
+  uint32_t err;
+  uint32_t carry_outs;
+  int lane, team;
+};
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CFR_SYNC() __syncthreads()
+#else
+#define CFR_SYNC() ((void)0)
+#endif
+
+CIT_HD uint32_t* row_of(const CfrTree& T, int id) { return T.rows + (long)id * (CIT_GAME_BYTES / 4); }
+// deepcopy(game): the team copies one row
+CIT_HD void copy_row(const CfrTree& T, uint32_t* dst, const uint32_t* src) {
+  CFR_SYNC();
+  for (int i = T.lane; i < CIT_GAME_BYTES / 4; i += T.team) dst[i] = src[i];
+  CFR_SYNC();
+}
+
+// ------------------------------------------------------------ numpy fp64
+// np.sum of a 1-D float64 run (numpy pairwise_sum); `at(i)` yields element i.
+template <class At>
+CIT_HD double np_leaf_sum(At at, int lo, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; i++) r += at(lo + i);
+    return r;
+  }
+  double r[8];
+  for (int j = 0; j < 8; j++) r[j] = at(lo + j);
+  int i = 8;
+  for (; i < n - n % 8; i += 8)
+    for (int j = 0; j < 8; j++) r[j] += at(lo + i + j);
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += at(lo + i);
+  return res;
+}
+template <int D, class At>
+CIT_HD double np_sum_rec(At at, int lo, int n, uint32_t& err) {
+  if (n <= 128) return np_leaf_sum(at, lo, n);
+  if constexpr (D == 0) {
+    err |= CIT_ERR_OVERFLOW;
+    return 0.0;
+  } else {
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_sum_rec<D - 1>(at, lo, n2, err) + np_sum_rec<D - 1>(at, lo + n2, n - n2, err);
+  }
+}
+template <class At>
+CIT_HD double np_sum(At at, int n, uint32_t& err) { return np_sum_rec<5>(at, 0, n, err); }
+
+// RandomState.choice(range(n), p=p) (legacy): ValueError -> err, returns -1.
+template <class P>
+CIT_HD int np_choice(CitMT& rng, P p, int n, uint32_t& err) {
+  if (n <= 0) { err |= CIT_ERR_VALUE; return -1; }
+  double s = p(0), c = 0.0;
+  for (int i = 0; i < n; i++) {
+    double v = p(i);
+    if (v != v || v < 0) { err |= CIT_ERR_VALUE; return -1; }
+    if (i) {
+      double y = v - c, t = s + y;
+      c = (t - s) - y;
+      s = t;
+    }
+  }
+  if (fabs(s - 1.0) > CFR_ATOL) { err |= CIT_ERR_VALUE; return -1; }
+  double tot = 0.0;
+  for (int i = 0; i < n; i++) tot = i ? tot + p(i) : p(0);
+  double u = mt_random(rng);
+  double cum = 0.0;
+  int idx = 0;
+  for (int i = 0; i < n; i++) {
+    cum = i ? cum + p(i) : p(0);
+    if (cum / tot <= u) idx = i + 1;
+  }
+  return idx < n ? idx : n - 1;
+}
+CIT_HD int np_choice_uniform(CitMT& rng, int n, uint32_t& err) {
+  double q = n > 0 ? 1.0 / n : 0.0;
+  return np_choice(rng, [q](int) { return q; }, n, err);
+}
+
+// ------------------------------------------------------- option equality
+// A fingerprint of a card-type sequence (Card tuples compare by type, in order).
+CIT_HD uint64_t type_seq_hash(uint64_t h, int t) { return (h ^ (uint64_t)(t + 1)) * 0x100000001B3ull; }
+
+// The form an opponent child's option is stored and compared in
+// (option.__eq__, option.py:14-15): list-valued attributes become type-sequence
+// fingerprints, empty_option's next_gamestate its (state, player) (GameState.__eq__).
+CIT_HD CitOpt opt_key(const CitOpt& o, const CitGame& g) {
+  CitOpt k = o;
+  const CitPlayer& P = g.pl[o.perp];
+  uint64_t h = 0xcbf29ce484222325ull;
+  switch (o.name) {
+    case O_EMPTY:
+      k.b = o.a == 0 ? 5 : g.nx_state;
+      k.c = (uint8_t)(o.a == 0 ? o.perp : g.nx_pid);
+      break;
+    case O_DISCARD_AND_DRAW:
+    case O_CARDINAL:
+      for (int i = 0; i < P.n_hand; i++)
+        if ((o.x >> i) & 1) h = type_seq_hash(h, card_type(P.hand[i]));
+      k.x = h;
+      break;
+    case O_SCHOLAR_PICK:
+      for (int i = 0; i < g.n_seven; i++) h = type_seq_hash(h, card_type(g.seven[i]));
+      k.x = h;
+      break;
+    case O_GIVE_BACK_CARD: {   // dict equality: order-free over (pid, type)
+      uint64_t acc = 0;
+      for (int i = 0; i < o.b; i++)
+        acc += type_seq_hash(type_seq_hash(h, g.seer_from[i]), card_type((int)((o.x >> (8 * i)) & 0xFF)));
+      k.x = acc;
+      break;
+    }
+    default:
+      break;
+  }
+  return k;
+}
+CIT_HD bool opt_eq(const CitOpt& p, const CitOpt& q) {
+  if (p.name != q.name || p.perp != q.perp || p.target != q.target) return false;
+  switch (p.name) {
+    case O_WHICH_CARD:
+      return card_type(p.a) == card_type(q.a) && (p.b == CIT_NO_CARD) == (q.b == CIT_NO_CARD) &&
+             (p.b == CIT_NO_CARD || card_type(p.b) == card_type(q.b)) && p.flags == q.flags;
+    case O_BUILD:
+      return card_type(p.a) == card_type(q.a) && p.c == q.c;
+    case O_LAB: case O_LIGHTHOUSE: case O_MUSEUM: case O_WEAPON_STORAGE: case O_WARLORD: case O_MARSHAL:
+      return card_type(p.a) == card_type(q.a);
+    case O_TAKE_FROM_HAND:
+      return p.flags == q.flags && card_type(p.a) == card_type(q.a) && (!(p.flags & OF_BUILD) || p.c == q.c);
+    case O_DIPLOMAT:
+      return card_type(p.a) == card_type(q.a) && card_type(p.b) == card_type(q.b) && p.c == q.c;
+    case O_EMPTY:
+      return p.b == q.b && p.c == q.c;
+    case O_SCHOLAR_PICK:
+      return card_type(p.a) == card_type(q.a) && p.x == q.x;
+    case O_DISCARD_AND_DRAW:
+      return p.x == q.x;
+    case O_CARDINAL:
+      return card_type(p.a) == card_type(q.a) && p.x == q.x && p.c == q.c && p.flags == q.flags;
+    case O_GIVE_BACK_CARD:
+      return p.b == q.b && p.x == q.x;
+    default:
+      return p.a == q.a && p.b == q.b && p.c == q.c && p.flags == q.flags && p.x == q.x;
+  }
+}
+
+// take_from_hand builds: carry_out_wizard_take_from_hand overwrites the
+// option's `replica` with the count already built (option_functions.py:317);
+// the stored child option keeps the overwritten value.
+CIT_HD void opt_mutate(CitOpt& o, const CitGame& g) {
+  if (o.name == O_TAKE_FROM_HAND && (o.flags & OF_BUILD))
+    o.c = (uint8_t)count_type(g.pl[o.perp].build, g.pl[o.perp].n_build, card_type(o.a));
+}
+
+// -------------------------------------------------------------- nodes
+CIT_HD void tree_carry(CfrTree& T, CitGame& g, const CitOpt& o, int& winner) {
+  winner = cit_carry_out(g, o, T.py);
+  T.carry_outs++;
+}
+
+// CFRNode(game=w, parent, depth): skip_false_choice on w, then a new node
+// whose row is w.  Returns the node id (-1 on error).
+CIT_HD int cfr_node(CfrTree& T, CitGame& w, int parent, int depth) {
+  uint32_t e = 0;
+  cit_prepare_options(w, T.py, T.seer);
+  int n = cit_count_options(w, e, T.seer);
+  int i = 0;
+  bool done = false;
+  while (n == 1 && !done && !e && !w.err) {
+    i++;
+    CitOpt o = cit_pick_option(w, 0, T.seer);
+    int win;
+    tree_carry(T, w, o, win);
+    done = win >= 0;
+    cit_prepare_options(w, T.py, T.seer);
+    n = cit_count_options(w, e, T.seer);
+    if (i > 100) done = true;
+  }
+  T.err |= e | w.err;
+  if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+  int id = T.n_nodes++;
+  CfrNode& N = T.nodes[id];
+  N.parent = parent;
+  N.first_edge = -1;
+  N.n_children = 0;
+  N.edge_cap = 0;
+  N.depth = (int16_t)depth;
+  N.player = w.gs_pid;
+  N.gs_state = (int8_t)w.gs_state;
+  N.flags = (uint8_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0));
+  N.winner = w.winner;
+  for (int k = 0; k < 6; k++) N.nv[k] = N.wp[k] = N.pred[k] = 0.0;
+  copy_row(T, row_of(T, id), reinterpret_cast<const uint32_t*>(&w));
+  return id;
+}
+
+CIT_HD int alloc_edges(CfrTree& T, int n) {
+  if (T.n_edges + n > T.edge_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+  int f = T.n_edges;
+  T.n_edges += n;
+  return f;
+}
+CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
+  E.opt = o;
+  E.child = child;
+  for (int k = 0; k < 6; k++) E.R[k] = E.S[k] = E.CS[k] = 0.0;
+}
+
+// ------------------------------------------------------------ expansion
+CIT_HD void cfr_expand_role_pick(CfrTree& T, int n) {            // :102-131
+  int f = alloc_edges(T, CFR_ROLE_CHILDREN);
+  if (f < 0) return;
+  T.nodes[n].first_edge = f;
+  T.nodes[n].edge_cap = CFR_ROLE_CHILDREN;
+  int depth = T.nodes[n].depth + 1;
+  for (int r = 0; r < CFR_ROLE_CHILDREN && !T.err; r++) {
+    copy_row(T, reinterpret_cast<uint32_t*>(T.w1), row_of(T, n));
+    CitGame& h = *T.w1;
+    CitOpt last = mk(O_NUM_NAMES, 0);
+    int guard = 0;
+    while (h.gs_state != 1 && !T.err) {
+      uint32_t e = 0;
+      cit_prepare_options(h, T.py, T.seer);
+      int cnt = cit_count_options(h, e, T.seer);
+      T.err |= e;
+      int k = np_choice_uniform(T.np, cnt, T.err);
+      if (T.err) break;
+      last = cit_pick_option(h, k, T.seer);
+      int win;
+      tree_carry(T, h, last, win);
+      T.err |= h.err;
+      if (++guard > 64) T.err |= CIT_ERR_UNSUPPORTED;
+    }
+    if (T.err) return;
+    int c = cfr_node(T, h, n, depth);
+    if (c < 0) return;
+    init_edge(T.edges[f + r], last, c);
+    T.nodes[n].n_children = (int16_t)(r + 1);
+  }
+}
+
+CIT_HD void cfr_expand_own(CfrTree& T, int n) {                   // :133-151
+  CitGame& g = *T.w0;
+  copy_row(T, reinterpret_cast<uint32_t*>(&g), row_of(T, n));
+  cit_prepare_options(g, T.py, T.seer);
+  ListSink s(T.optbuf, CFR_OPT_CAP);
+  cit_enum_options(g, s, T.seer);
+  T.err |= s.err | g.err;
+  if (s.n > CFR_OPT_CAP) T.err |= CIT_ERR_OVERFLOW;
+  copy_row(T, row_of(T, n), reinterpret_cast<const uint32_t*>(&g));   // get_options mutated the node's game
+  if (T.err) return;
+  int cnt = s.n;
+  int f = alloc_edges(T, cnt);
+  if (f < 0) return;
+  CfrNode& N = T.nodes[n];
+  N.first_edge = f;
+  N.edge_cap = (int16_t)cnt;
+  int par = N.parent;
+  bool sample = par < 0 || N.player != T.nodes[par].player;
+  bool role_sample = par >= 0 && T.nodes[par].gs_state != 0;
+  int depth = N.depth + 1;
+  for (int i = 0; i < cnt && !T.err; i++) {
+    CitOpt o = T.optbuf[i];
+    copy_row(T, reinterpret_cast<uint32_t*>(T.w1), reinterpret_cast<const uint32_t*>(&g));
+    CitGame& h = *T.w1;
+    if (sample) cit_sample_private(h, T.orig, role_sample, T.py, T.tmp);
+    opt_mutate(o, h);
+    int win;
+    tree_carry(T, h, o, win);
+    T.err |= h.err;
+    if (T.err) return;
+    int c = cfr_node(T, h, n, depth);
+    if (c < 0) return;
+    init_edge(T.edges[f + i], o, c);
+    T.nodes[n].n_children = (int16_t)(i + 1);
+  }
+}
+
+CIT_HD void cfr_expand_opponent(CfrTree& T, int n) {              // :153-179
+  CfrNode& N = T.nodes[n];
+  copy_row(T, reinterpret_cast<uint32_t*>(T.w1), row_of(T, n));
+  CitGame& h = *T.w1;
+  int par = N.parent;
+  if (par < 0 || N.player != T.nodes[par].player)
+    cit_sample_private(h, T.orig, par >= 0 && T.nodes[par].gs_state != 0, T.py, T.tmp);
+  uint32_t e = 0;
+  cit_prepare_options(h, T.py, T.seer);
+  int cnt = cit_count_options(h, e, T.seer);
+  T.err |= e | h.err;
+  int k = np_choice_uniform(T.np, cnt, T.err);
+  if (T.err) return;
+  CitOpt o = cit_pick_option(h, k, T.seer);
+  opt_mutate(o, h);
+  CitOpt key = opt_key(o, h);
+  int win;
+  tree_carry(T, h, o, win);
+  T.err |= h.err;
+  if (T.err) return;
+  for (int j = 0; j < N.n_children; j++)
+    if (opt_eq(T.edges[N.first_edge + j].opt, key)) return;
+  if (N.first_edge < 0) {
+    int f = alloc_edges(T, CFR_OPP_CHILDREN);
+    if (f < 0) return;
+    N.first_edge = f;
+    N.edge_cap = CFR_OPP_CHILDREN;
+  }
+  int c = cfr_node(T, h, n, N.depth + 1);
+  if (c < 0) return;
+  init_edge(T.edges[T.nodes[n].first_edge + T.nodes[n].n_children], key, c);
+  T.nodes[n].n_children++;
+}
+
+CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
+  CfrNode& N = T.nodes[n];
+  if (N.gs_state == 0 && N.n_children == 0) {
+    N.flags |= NF_ROLE_PICK;
+    cfr_expand_role_pick(T, n);
+  } else if (N.player == T.orig && N.n_children == 0) {
+    cfr_expand_own(T, n);
+  } else if (N.player != T.orig && N.n_children < CFR_OPP_CHILDREN) {
+    cfr_expand_opponent(T, n);
+  }
+}
+
+// ---------------------------------------------------------- strategies
+CIT_HD void cfr_update_strategy(CfrTree& T, int n) {               // :292-319
+  CfrNode& N = T.nodes[n];
+  int nch = N.n_children;
+  if (nch == 0) return;
+  CfrEdge* E = T.edges + N.first_edge;
+  if (!(N.flags & NF_ROLE_PICK)) {
+    for (int a = 0; a < nch; a++) E[a].S[0] = exp((-E[a].R[0]) * CFR_LN13);
+    double tot = np_sum([E](int i) { return E[i].S[0]; }, nch, T.err);
+    for (int a = 0; a < nch; a++) E[a].S[0] = tot > 0 ? E[a].S[0] / tot : 1.0 / nch;
+    for (int a = 0; a < nch; a++) E[a].CS[0] += E[a].S[0];
+    double cs = np_sum([E](int i) { return E[i].CS[0]; }, nch, T.err);
+    for (int a = 0; a < nch; a++) E[a].CS[0] = E[a].CS[0] / cs;
+  } else {
+    // role pick: [6 players, nch] arrays; totals along players (axis 0, sequential)
+    double tots[CFR_ROLE_CHILDREN];
+    bool small = false;
+    for (int a = 0; a < nch; a++) {
+      double tot = 0.0;
+      for (int p = 0; p < 6; p++) {
+        E[a].S[p] = exp((-E[a].R[p]) * CFR_LN13);
+        tot = p ? tot + E[a].S[p] : E[a].S[0];
+      }
+      tots[a] = tot;
+      small |= tot <= 1e-8;
+    }
+    for (int a = 0; a < nch; a++)
+      for (int p = 0; p < 6; p++) {
+        double v = E[a].S[p] / tots[a];
+        E[a].S[p] = small ? (tots[a] > 1e-8 ? v : 1.0 / 6) : v;
+      }
+    for (int a = 0; a < nch; a++)
+      for (int p = 0; p < 6; p++) E[a].CS[p] += E[a].S[p];
+    double cs = np_sum([E](int i) { return E[i / 6].CS[i % 6]; }, nch * 6, T.err);
+    for (int a = 0; a < nch; a++)
+      for (int p = 0; p < 6; p++) E[a].CS[p] = E[a].CS[p] / cs;
+  }
+}
+
+// action_choice(live=False) (:67-91): returns the edge index within the node
+CIT_HD int cfr_choose(CfrTree& T, int n) {
+  CfrNode& N = T.nodes[n];
+  int nch = N.n_children;
+  const CfrEdge* E = T.edges + (N.first_edge < 0 ? 0 : N.first_edge);
+  if (!(N.flags & NF_ROLE_PICK)) {
+    double tot = np_sum([E](int i) { return E[i].CS[0]; }, nch, T.err);
+    return np_choice(T.np, [E, tot](int i) { return E[i].CS[0] / tot; }, nch, T.err);
+  }
+  // weighted_average_strategy (:51-65) over turn_orders_for_roles of the node's game
+  const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
+  if (nch > CFR_ROLE_CHILDREN) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+  double w[CFR_ROLE_CHILDREN];
+  int hs = 0;
+  for (int i = 0; i < CIT_NP; i++) hs += g.turn[i];
+  for (int a = 0; a < nch; a++) {
+    double acc = 0.0;
+    for (int i = 0; i < CIT_NP; i++) acc += E[a].CS[g.turn[i]] * (double)(CIT_NP - i);
+    w[a] = acc / (double)hs;
+  }
+  double s = np_sum([&w](int i) { return w[i]; }, nch, T.err);
+  if (s == 0.0) return np_choice_uniform(T.np, nch, T.err);
+  return np_choice(T.np, [&w, s](int i) { return w[i] / s; }, nch, T.err);
+}
+
+// ------------------------------------------------------------- backup
+CIT_HD void cfr_update_regrets(CfrTree& T, int n) {                // :231-256
+  CfrNode& N = T.nodes[n];
+  CfrEdge* E = T.edges + N.first_edge;
+  int nch = N.n_children;
+  if (!(N.flags & NF_ROLE_PICK)) {
+    int p = N.player;
+    double mx = T.nodes[E[0].child].wp[p];
+    for (int a = 1; a < nch; a++) {
+      double v = T.nodes[E[a].child].wp[p];
+      if (v > mx) mx = v;
+    }
+    for (int a = 0; a < nch; a++) E[a].R[0] += mx - T.nodes[E[a].child].wp[p];
+  } else {
+    for (int a = 0; a < nch; a++) {
+      const double* wp = T.nodes[E[a].child].wp;
+      double mx = wp[0];
+      for (int p = 1; p < 6; p++) mx = (mx != mx || wp[p] != wp[p]) ? NAN : (wp[p] > mx ? wp[p] : mx);
+      for (int p = 0; p < 6; p++) E[a].R[p] += mx - wp[p];
+    }
+  }
+}
+
+CIT_HD void cfr_backprop(CfrTree& T, int n, const double* reward, bool model) {   // :276-290
+  while (n >= 0) {
+    CfrNode& N = T.nodes[n];
+    double s0 = 0.0;
+    for (int k = 0; k < 6; k++) s0 += N.nv[k];
+    if (T.training || s0 == 0.0 || !model)
+      for (int k = 0; k < 6; k++) N.nv[k] += reward[k];
+    double s = 0.0;
+    for (int k = 0; k < 6; k++) s += N.nv[k];
+    for (int k = 0; k < 6; k++) N.wp[k] = N.nv[k] / s;
+    if (N.n_children) cfr_update_regrets(T, n);
+    n = N.parent;
+  }
+}
+
+// ---------------------------------------------------------------- drivers
+// cfr_train(iters) on the game in T.w0 (the root's game: skip_false_choice
+// mutates it, as the reference mutates the game passed to CFRNode).
+// Returns the root id.
+CIT_HD int cfr_train(CfrTree& T, int iters) {
+  int root = cfr_node(T, *T.w0, -1, 0);
+  if (root < 0 || T.err) return root;
+  if (T.nodes[root].flags & NF_TERMINAL) return root;
+  cfr_expand(T, root);
+  int n = root;
+  for (int it = 0; it < iters && !T.err; it++) {
+    cfr_update_strategy(T, n);
+    int a = cfr_choose(T, n);
+    if (T.err) break;
+    n = T.edges[T.nodes[n].first_edge + a].child;
+    if (T.nodes[n].flags & NF_TERMINAL) {
+      double rw[6] = {0, 0, 0, 0, 0, 0};
+      if (T.nodes[n].winner >= 0) rw[T.nodes[n].winner] = 1.0;
+      cfr_backprop(T, n, rw, false);
+      cfr_update_strategy(T, n);
+      n = root;
+    } else {
+      cfr_expand(T, n);
+    }
+  }
+  if (!T.err) cfr_update_strategy(T, root);
+  return root;
+}
+
+// action_choice(live=True) at the root (:67-91; game.py:312-317 for a role pick).
+CIT_HD CitOpt cfr_live_choice(CfrTree& T, int root) {
+  CfrNode& N = T.nodes[root];
+  if (!(N.flags & NF_ROLE_PICK)) {
+    int a = cfr_choose(T, root);
+    if (T.err || a < 0) return mk(O_NUM_NAMES, 0);
+    return T.edges[N.first_edge + a].opt;
+  }
+  CitGame& g = *T.w0;
+  copy_row(T, reinterpret_cast<uint32_t*>(&g), row_of(T, root));
+  cit_prepare_options(g, T.py, T.seer);
+  ListSink s(T.optbuf, CFR_OPT_CAP);
+  cit_enum_options(g, s, T.seer);
+  T.err |= s.err;
+  int pid = g.gs_pid;
+  const CfrEdge* E = T.edges + N.first_edge;
+  double sum = 0.0;
+  for (int j = 0; j < s.n; j++) sum += E[T.optbuf[j].a].S[pid];
+  int j = np_choice(T.np, [&](int i) { return E[T.optbuf[i].a].S[pid] / sum; }, s.n, T.err);
+  copy_row(T, row_of(T, root), reinterpret_cast<const uint32_t*>(&g));
+  if (T.err || j < 0) return mk(O_NUM_NAMES, 0);
+  return T.optbuf[j];
+}

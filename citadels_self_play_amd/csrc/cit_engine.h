@@ -1445,6 +1445,137 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
   return w;
 }
 
+// ================================================= determinization
+// remove_role_from_role_knowledge (game.py:298-301) on a copied knowledge row:
+// drop `role` (by name, i.e. by role index) from every unconfirmed entry.
+CIT_HD void kr_strip(const CitGame& g, uint16_t* kr, int role) {
+  for (int j = 0; j < CIT_NP; j++) {
+    if (kr[j] & KR_CONFIRMED) continue;
+    for (int rid = -1; rid < 8; rid++)
+      if (role_of_id(g, rid) == role) kr[j] &= (uint16_t)~(1u << (rid + 1));
+  }
+}
+
+// Game.sample_private_information(players[orig], role_sample) (game.py:215-339):
+// resample everything `orig` cannot see.  `unk` is >= CIT_USED_CAP bytes of
+// scratch (LDS on the device).
+CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rng, uint8_t* unk) {
+  CitPlayer& PC = g.pl[orig];
+  // hk.used with probability (confidence-1)*0.2 (:217-222)
+  for (int e = 0; e < g.n_kh; e++) {
+    CitKH& k = g.kh[e];
+    if (k.owner != orig) continue;
+    double r = mt_random(rng);
+    bool used = (double)(kh_conf(k) - 1) * 0.2 > r;
+    k.conf_flags = (uint8_t)((k.conf_flags & ~0x20) | (used ? 0x20 : 0));
+  }
+  // get_unknown_cards (:183-213)
+  uint8_t nu = g.n_used_cards;
+  for (int i = 0; i < nu; i++) unk[i] = g.used_cards[i];
+  for (int p = 0; p < CIT_NP; p++)
+    for (int i = 0; i < g.pl[p].n_build; i++) take_like(unk, nu, g.pl[p].build[i]);
+  for (int p = 0; p < CIT_NP; p++)
+    for (int i = 0; i < g.pl[p].n_museum; i++) take_like(unk, nu, g.pl[p].museum[i]);
+  for (int i = 0; i < PC.n_hand; i++) take_like(unk, nu, PC.hand[i]);
+  {
+    int off = 0;
+    for (int e = 0; e < g.n_kh; e++) {
+      const CitKH& k = g.kh[e];
+      if (k.owner == orig && (k.conf_flags & 0x20))
+        for (int i = 0; i < k.len; i++) take_like(unk, nu, g.kh_pool[off + i]);
+      off += k.len;
+    }
+  }
+  // sample_deck (:245-262): lighthouse knowledge first, then shuffled unknowns
+  {
+    int n = g.n_deck;
+    int lo = -1, ll = 0, off = 0;
+    for (int e = 0; e < g.n_kh; e++) {
+      const CitKH& k = g.kh[e];
+      if (k.owner == orig && k.target == -1 && (k.conf_flags & 0x20)) { lo = off; ll = k.len; break; }
+      off += k.len;
+    }
+    g.n_deck = 0;
+    g.deck_head = 0;
+    if (lo >= 0) {
+      int kk = ll < n ? ll : n;
+      for (int i = 0; i < kk; i++) deck_put(g, g.kh_pool[lo + i]);
+      n -= kk;
+    }
+    shuffle_arr(rng, unk, nu);
+    for (int i = 0; i < n; i++) deck_put(g, pop_front(unk, nu));
+  }
+  // sample_warrants_and_blackmails (:321-336)
+  for (int which = 0; which < 2; which++) {
+    int shift = which == 0 ? RP_BLACKMAIL_SHIFT : RP_WARRANT_SHIFT;
+    uint8_t ks[8];
+    int nk = 0;
+    for (int r = 0; r < 8; r++)
+      if ((g.rp[r] >> shift) & 3) ks[nk++] = (uint8_t)r;
+    if (!nk) continue;
+    shuffle_arr(rng, ks, nk);
+    for (int i = 0; i < nk; i++) {
+      int r = ks[i];
+      g.rp[r] = (uint8_t)((g.rp[r] & ~(3u << shift)) | ((r == ks[0] ? WB_REAL : WB_FAKE) << shift));
+    }
+  }
+  uint16_t kr[CIT_NP];
+  for (int j = 0; j < CIT_NP; j++) kr[j] = PC.kr[j];
+  if (role_sample) {   // remove_role_and_smaller_id_roles_from_role_knowledge_if_unconfirmed (:304-310)
+    int role = g.pl[g.gs_pid].role;
+    kr_strip(g, kr, role);
+    if (role != ROLE_NONE) {
+      int rr = role_rank(g, role);
+      for (int rid = 0; rid < 8; rid++)
+        if (rid < rr) kr_strip(g, kr, g.roles[rid]);
+    }
+  }
+  for (int p = 0; p < CIT_NP; p++) {
+    CitPlayer& Q = g.pl[p];
+    if (p != orig) {   // sample_cards_for_opponent (:264-280)
+      int n = Q.n_hand, ho = -1, hl = 0, off = 0;
+      for (int e = 0; e < g.n_kh; e++) {
+        const CitKH& k = g.kh[e];
+        if (k.owner == orig && k.target == p && (k.conf_flags & 0x20)) { ho = off; hl = k.len; break; }
+        off += k.len;
+      }
+      Q.n_hand = 0;
+      if (ho >= 0) {
+        int kk = hl < n ? hl : n;
+        for (int i = 0; i < kk; i++) put_card(g, HAND(Q), g.kh_pool[ho + i]);
+        n -= kk;
+      }
+      for (int i = 0; i < n; i++) put_card(g, HAND(Q), pop_front(unk, nu));
+    }
+    // sample_roles_for_opponent (:283-295)
+    if (role_sample && p != orig && p != g.gs_pid && g.gs_state != 0) {
+      int cnt = 0;
+      for (int rid = -1; rid < 8; rid++) cnt += (kr[p] >> (rid + 1)) & 1;
+      int k = (int)mt_randbelow(rng, (uint32_t)cnt);
+      if (cnt) {
+        int rid = -1;
+        for (int q = -1; q < 8; q++)
+          if ((kr[p] >> (q + 1)) & 1) {
+            if (k == 0) { rid = q; break; }
+            k--;
+          }
+        Q.role = (uint8_t)role_of_id(g, rid);
+        kr_strip(g, kr, Q.role);
+      } else {   // the IndexError band-aid: first role id not in used_roles
+        int pick = -1;
+        for (int rid = 0; rid < 8 && pick < 0; rid++) {
+          bool in = false;
+          for (int u = 0; u < g.n_used_roles && u < CIT_NP; u++) in |= g.used_roles[u] == rid;
+          if (!in) pick = rid;
+        }
+        if (pick < 0) { g.err |= CIT_ERR_INDEX; return; }   // StopIteration
+        Q.role = g.roles[pick];
+      }
+    }
+  }
+  if (role_sample && g.gs_state != 0) refresh_used_roles(g);
+}
+
 // One random-policy step (compare_to_random.py:37-39): get_options ->
 // random.choice -> carry_out.  Returns 1 when the lane is done (winner or error).
 CIT_HD int cit_random_step(CitGame& g, CitMT& rng, uint64_t* seer) {

@@ -8,7 +8,9 @@
 #include <stddef.h>
 #include <string.h>
 
-#include "cit_engine.h"
+#include <stdlib.h>
+
+#include "cit_cfr.h"
 
 extern "C" {
 
@@ -116,6 +118,78 @@ void cith_rollout(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B
     winner[l] = g[l].winner;
     SAVE(r);
   }
+}
+
+// config-3 position harness: k = random.randint(lo, hi) random-policy steps
+// from the lane's own stream (stops at a winner)
+void cith_advance_random(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int lo, int hi, int* steps) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    int k = lo + (int)mt_randbelow(r, (uint32_t)(hi - lo + 1));
+    int s = 0;
+    while (s < k && !g[l].terminal && !g[l].err) {
+      cit_random_step(g[l], r, seer + (long)l * CIT_SEER_MAX);
+      s++;
+    }
+    steps[l] = s;
+    SAVE(r);
+  }
+}
+
+int cith_cfr_sizes(int* out) {
+  out[0] = (int)sizeof(CfrNode);
+  out[1] = (int)sizeof(CfrEdge);
+  out[2] = CFR_OPT_CAP;
+  return 3;
+}
+
+// run_mccfr(game, max_iterations=iters) without a model for every lane;
+// pool = per lane [node_cap CfrNode][edge_cap CfrEdge][node_cap rows].
+// stats[l] = {root, n_nodes, n_edges, carry_outs, err}
+void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx, uint64_t* seer, int B,
+                     int iters, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen, int* stats) {
+  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
+  CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
+  CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
+  uint8_t tmp[128];
+  for (int l = 0; l < B; l++) {
+    uint8_t* base = pool + per * l;
+    CfrTree T;
+    T.nodes = (CfrNode*)base;
+    T.edges = (CfrEdge*)(base + (long)node_cap * sizeof(CfrNode));
+    T.rows = (uint32_t*)(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
+    T.node_cap = node_cap;
+    T.edge_cap = edge_cap;
+    T.n_nodes = T.n_edges = 0;
+    T.orig = g[l].gs_pid;
+    T.training = false;
+    T.py = lane_rng(mt, idx, B, l);
+    T.np = lane_rng(npmt, npidx, B, l);
+    T.seer = seer + (long)l * CIT_SEER_MAX;
+    T.optbuf = optbuf + (long)l * CFR_OPT_CAP;
+    T.w0 = w0;
+    T.w1 = w1;
+    T.tmp = tmp;
+    T.err = 0;
+    T.carry_outs = 0;
+    T.lane = 0;
+    T.team = 1;
+    memcpy(w0, &g[l], CIT_GAME_BYTES);
+    int root = cfr_train(T, iters);
+    CitOpt c = mk(O_NUM_NAMES, 0);
+    if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
+    chosen[l] = c;
+    if (root >= 0) memcpy(&g[l], row_of(T, root), CIT_GAME_BYTES);
+    idx[l] = T.py.pos;
+    npidx[l] = T.np.pos;
+    stats[5 * l + 0] = root;
+    stats[5 * l + 1] = T.n_nodes;
+    stats[5 * l + 2] = T.n_edges;
+    stats[5 * l + 3] = (int)T.carry_outs;
+    stats[5 * l + 4] = (int)T.err;
+  }
+  free(w0);
+  free(w1);
 }
 
 }  // extern "C"

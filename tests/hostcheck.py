@@ -77,3 +77,53 @@ class HostBatch:
         lib().cith_rollout(_p(self.games), _p(self.mt), _p(self.idx), _p(self.seer), C.c_int(self.B), C.c_int(max_steps),
                            _p(steps), _p(w))
         return steps, w
+
+
+NODE_DT = np.dtype([("parent", "<i4"), ("first_edge", "<i4"), ("n_children", "<i2"), ("edge_cap", "<i2"),
+                    ("depth", "<i2"), ("player", "i1"), ("gs_state", "i1"), ("flags", "u1"), ("winner", "i1"),
+                    ("pad", "u1", 6), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
+EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8", 6), ("S", "<f8", 6),
+                    ("CS", "<f8", 6)])
+assert NODE_DT.itemsize == 168 and EDGE_DT.itemsize == 168
+
+
+def cfr_pool_bytes(node_cap, edge_cap):
+    return node_cap * 168 + edge_cap * 168 + node_cap * L.GAME_BYTES
+
+
+class HostCfr:
+    """Host-build MCCFR decisions over a HostBatch (config-3 harness)."""
+
+    def __init__(self, hb, node_cap=2048, edge_cap=4096):
+        self.hb = hb
+        B = hb.B
+        self.node_cap, self.edge_cap = node_cap, edge_cap
+        self.npmt = np.zeros((L.MT_N, B), np.uint32)
+        self.npidx = np.zeros(B, np.uint32)
+        lib().cith_mt_seed(_p(self.npmt), _p(self.npidx), C.c_int(B), _p(hb.seeds), C.c_int(1))
+        self.pool = np.zeros(B * cfr_pool_bytes(node_cap, edge_cap), np.uint8)
+        self.optbuf = np.zeros((B, 512, 16), np.uint8)
+
+    def advance(self, lo, hi):
+        steps = np.zeros(self.hb.B, np.int32)
+        hb = self.hb
+        lib().cith_advance_random(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(hb.seer), C.c_int(hb.B), C.c_int(lo),
+                                  C.c_int(hi), _p(steps))
+        return steps
+
+    def decide(self, iters):
+        hb = self.hb
+        chosen = np.zeros((hb.B, 16), np.uint8)
+        stats = np.zeros((hb.B, 5), np.int32)
+        lib().cith_cfr_decide(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(self.npmt), _p(self.npidx), _p(hb.seer),
+                              C.c_int(hb.B), C.c_int(iters), _p(self.pool), C.c_int(self.node_cap),
+                              C.c_int(self.edge_cap), _p(self.optbuf), _p(chosen), _p(stats))
+        return chosen, stats
+
+    def tree(self, l):
+        per = cfr_pool_bytes(self.node_cap, self.edge_cap)
+        base = self.pool[l * per:(l + 1) * per]
+        nodes = base[:self.node_cap * 168].view(NODE_DT)
+        edges = base[self.node_cap * 168:self.node_cap * 168 + self.edge_cap * 168].view(EDGE_DT)
+        rows = base[self.node_cap * 168 + self.edge_cap * 168:].reshape(self.node_cap, L.GAME_BYTES)
+        return nodes, edges, rows

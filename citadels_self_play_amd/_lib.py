@@ -28,6 +28,10 @@ _SIGS = {
     "cit_random_choice": ([vp, vp, vp, i32, vp, i32, vp, vp, vp, vp], i32),
     "cit_carry_out": ([vp, vp, vp, i32, vp, vp, vp], i32),
     "cit_rollout_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
+    "cit_cfr_pool_bytes": ([i32, i32], i32),
+    "cit_cfr_opt_cap": ([], i32),
+    "cit_advance_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp], i32),
+    "cit_cfr_decide": ([vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, vp], i32),
 }
 
 

@@ -75,9 +75,34 @@ struct CfrTree {
 #define CFR_SYNC() ((void)0)
 #endif
 
+// One out-of-line copy of each engine entry point for the search: the
+// engine is force-inlined by default (the rollout kernel wants that), and
+// inlining it at every call site of the search multiplies code size and
+// compile time.  The search reaches LDS rows through flat pointers here.
+#if defined(__HIPCC__)
+#define CIT_NOINLINE __host__ __device__ __attribute__((noinline))
+#else
+#define CIT_NOINLINE inline
+#endif
+CIT_NOINLINE int eng_carry(CitGame& g, const CitOpt& o, CitMT& r) { return cit_carry_out(g, o, r); }
+CIT_NOINLINE void eng_prepare(CitGame& g, CitMT& r, uint64_t* seer) { cit_prepare_options(g, r, seer); }
+CIT_NOINLINE int eng_count(const CitGame& g, uint32_t& err, const uint64_t* seer) {
+  return cit_count_options(g, err, seer);
+}
+CIT_NOINLINE CitOpt eng_pick(const CitGame& g, int k, const uint64_t* seer) { return cit_pick_option(g, k, seer); }
+CIT_NOINLINE int eng_list(const CitGame& g, CitOpt* buf, int cap, uint32_t& err, const uint64_t* seer) {
+  ListSink s(buf, cap);
+  cit_enum_options(g, s, seer);
+  err |= s.err;
+  return s.n;
+}
+CIT_NOINLINE void eng_sample(CitGame& g, int orig, bool role_sample, CitMT& r, uint8_t* unk) {
+  cit_sample_private(g, orig, role_sample, r, unk);
+}
+
 CIT_HD uint32_t* row_of(const CfrTree& T, int id) { return T.rows + (long)id * (CIT_GAME_BYTES / 4); }
 // deepcopy(game): the team copies one row
-CIT_HD void copy_row(const CfrTree& T, uint32_t* dst, const uint32_t* src) {
+CIT_NOINLINE void copy_row(const CfrTree& T, uint32_t* dst, const uint32_t* src) {
   CFR_SYNC();
   for (int i = T.lane; i < CIT_GAME_BYTES / 4; i += T.team) dst[i] = src[i];
   CFR_SYNC();
@@ -223,27 +248,27 @@ CIT_HD void opt_mutate(CitOpt& o, const CitGame& g) {
 }
 
 // -------------------------------------------------------------- nodes
-CIT_HD void tree_carry(CfrTree& T, CitGame& g, const CitOpt& o, int& winner) {
-  winner = cit_carry_out(g, o, T.py);
+CIT_NOINLINE void tree_carry(CfrTree& T, CitGame& g, const CitOpt& o, int& winner) {
+  winner = eng_carry(g, o, T.py);
   T.carry_outs++;
 }
 
 // CFRNode(game=w, parent, depth): skip_false_choice on w, then a new node
 // whose row is w.  Returns the node id (-1 on error).
-CIT_HD int cfr_node(CfrTree& T, CitGame& w, int parent, int depth) {
+CIT_NOINLINE int cfr_node(CfrTree& T, CitGame& w, int parent, int depth) {
   uint32_t e = 0;
-  cit_prepare_options(w, T.py, T.seer);
-  int n = cit_count_options(w, e, T.seer);
+  eng_prepare(w, T.py, T.seer);
+  int n = eng_count(w, e, T.seer);
   int i = 0;
   bool done = false;
   while (n == 1 && !done && !e && !w.err) {
     i++;
-    CitOpt o = cit_pick_option(w, 0, T.seer);
+    CitOpt o = eng_pick(w, 0, T.seer);
     int win;
     tree_carry(T, w, o, win);
     done = win >= 0;
-    cit_prepare_options(w, T.py, T.seer);
-    n = cit_count_options(w, e, T.seer);
+    eng_prepare(w, T.py, T.seer);
+    n = eng_count(w, e, T.seer);
     if (i > 100) done = true;
   }
   T.err |= e | w.err;
@@ -277,7 +302,7 @@ CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
 }
 
 // ------------------------------------------------------------ expansion
-CIT_HD void cfr_expand_role_pick(CfrTree& T, int n) {            // :102-131
+CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T, int n) {            // :102-131
   int f = alloc_edges(T, CFR_ROLE_CHILDREN);
   if (f < 0) return;
   T.nodes[n].first_edge = f;
@@ -290,12 +315,12 @@ CIT_HD void cfr_expand_role_pick(CfrTree& T, int n) {            // :102-131
     int guard = 0;
     while (h.gs_state != 1 && !T.err) {
       uint32_t e = 0;
-      cit_prepare_options(h, T.py, T.seer);
-      int cnt = cit_count_options(h, e, T.seer);
+      eng_prepare(h, T.py, T.seer);
+      int cnt = eng_count(h, e, T.seer);
       T.err |= e;
       int k = np_choice_uniform(T.np, cnt, T.err);
       if (T.err) break;
-      last = cit_pick_option(h, k, T.seer);
+      last = eng_pick(h, k, T.seer);
       int win;
       tree_carry(T, h, last, win);
       T.err |= h.err;
@@ -309,17 +334,17 @@ CIT_HD void cfr_expand_role_pick(CfrTree& T, int n) {            // :102-131
   }
 }
 
-CIT_HD void cfr_expand_own(CfrTree& T, int n) {                   // :133-151
+CIT_NOINLINE void cfr_expand_own(CfrTree& T, int n) {                   // :133-151
   CitGame& g = *T.w0;
   copy_row(T, reinterpret_cast<uint32_t*>(&g), row_of(T, n));
-  cit_prepare_options(g, T.py, T.seer);
-  ListSink s(T.optbuf, CFR_OPT_CAP);
-  cit_enum_options(g, s, T.seer);
-  T.err |= s.err | g.err;
-  if (s.n > CFR_OPT_CAP) T.err |= CIT_ERR_OVERFLOW;
+  eng_prepare(g, T.py, T.seer);
+  uint32_t le = 0;
+  int nl = eng_list(g, T.optbuf, CFR_OPT_CAP, le, T.seer);
+  T.err |= le | g.err;
+  if (nl > CFR_OPT_CAP) T.err |= CIT_ERR_OVERFLOW;
   copy_row(T, row_of(T, n), reinterpret_cast<const uint32_t*>(&g));   // get_options mutated the node's game
   if (T.err) return;
-  int cnt = s.n;
+  int cnt = nl;
   int f = alloc_edges(T, cnt);
   if (f < 0) return;
   CfrNode& N = T.nodes[n];
@@ -333,7 +358,7 @@ CIT_HD void cfr_expand_own(CfrTree& T, int n) {                   // :133-151
     CitOpt o = T.optbuf[i];
     copy_row(T, reinterpret_cast<uint32_t*>(T.w1), reinterpret_cast<const uint32_t*>(&g));
     CitGame& h = *T.w1;
-    if (sample) cit_sample_private(h, T.orig, role_sample, T.py, T.tmp);
+    if (sample) eng_sample(h, T.orig, role_sample, T.py, T.tmp);
     opt_mutate(o, h);
     int win;
     tree_carry(T, h, o, win);
@@ -346,20 +371,20 @@ CIT_HD void cfr_expand_own(CfrTree& T, int n) {                   // :133-151
   }
 }
 
-CIT_HD void cfr_expand_opponent(CfrTree& T, int n) {              // :153-179
+CIT_NOINLINE void cfr_expand_opponent(CfrTree& T, int n) {              // :153-179
   CfrNode& N = T.nodes[n];
   copy_row(T, reinterpret_cast<uint32_t*>(T.w1), row_of(T, n));
   CitGame& h = *T.w1;
   int par = N.parent;
   if (par < 0 || N.player != T.nodes[par].player)
-    cit_sample_private(h, T.orig, par >= 0 && T.nodes[par].gs_state != 0, T.py, T.tmp);
+    eng_sample(h, T.orig, par >= 0 && T.nodes[par].gs_state != 0, T.py, T.tmp);
   uint32_t e = 0;
-  cit_prepare_options(h, T.py, T.seer);
-  int cnt = cit_count_options(h, e, T.seer);
+  eng_prepare(h, T.py, T.seer);
+  int cnt = eng_count(h, e, T.seer);
   T.err |= e | h.err;
   int k = np_choice_uniform(T.np, cnt, T.err);
   if (T.err) return;
-  CitOpt o = cit_pick_option(h, k, T.seer);
+  CitOpt o = eng_pick(h, k, T.seer);
   opt_mutate(o, h);
   CitOpt key = opt_key(o, h);
   int win;
@@ -393,7 +418,7 @@ CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
 }
 
 // ---------------------------------------------------------- strategies
-CIT_HD void cfr_update_strategy(CfrTree& T, int n) {               // :292-319
+CIT_NOINLINE void cfr_update_strategy(CfrTree& T, int n) {               // :292-319
   CfrNode& N = T.nodes[n];
   int nch = N.n_children;
   if (nch == 0) return;
@@ -432,7 +457,7 @@ CIT_HD void cfr_update_strategy(CfrTree& T, int n) {               // :292-319
 }
 
 // action_choice(live=False) (:67-91): returns the edge index within the node
-CIT_HD int cfr_choose(CfrTree& T, int n) {
+CIT_NOINLINE int cfr_choose(CfrTree& T, int n) {
   CfrNode& N = T.nodes[n];
   int nch = N.n_children;
   const CfrEdge* E = T.edges + (N.first_edge < 0 ? 0 : N.first_edge);
@@ -457,7 +482,7 @@ CIT_HD int cfr_choose(CfrTree& T, int n) {
 }
 
 // ------------------------------------------------------------- backup
-CIT_HD void cfr_update_regrets(CfrTree& T, int n) {                // :231-256
+CIT_NOINLINE void cfr_update_regrets(CfrTree& T, int n) {                // :231-256
   CfrNode& N = T.nodes[n];
   CfrEdge* E = T.edges + N.first_edge;
   int nch = N.n_children;
@@ -479,7 +504,7 @@ CIT_HD void cfr_update_regrets(CfrTree& T, int n) {                // :231-256
   }
 }
 
-CIT_HD void cfr_backprop(CfrTree& T, int n, const double* reward, bool model) {   // :276-290
+CIT_NOINLINE void cfr_backprop(CfrTree& T, int n, const double* reward, bool model) {   // :276-290
   while (n >= 0) {
     CfrNode& N = T.nodes[n];
     double s0 = 0.0;
@@ -524,7 +549,7 @@ CIT_HD int cfr_train(CfrTree& T, int iters) {
 }
 
 // action_choice(live=True) at the root (:67-91; game.py:312-317 for a role pick).
-CIT_HD CitOpt cfr_live_choice(CfrTree& T, int root) {
+CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T, int root) {
   CfrNode& N = T.nodes[root];
   if (!(N.flags & NF_ROLE_PICK)) {
     int a = cfr_choose(T, root);
@@ -533,15 +558,15 @@ CIT_HD CitOpt cfr_live_choice(CfrTree& T, int root) {
   }
   CitGame& g = *T.w0;
   copy_row(T, reinterpret_cast<uint32_t*>(&g), row_of(T, root));
-  cit_prepare_options(g, T.py, T.seer);
-  ListSink s(T.optbuf, CFR_OPT_CAP);
-  cit_enum_options(g, s, T.seer);
-  T.err |= s.err;
+  eng_prepare(g, T.py, T.seer);
+  uint32_t le = 0;
+  int nl = eng_list(g, T.optbuf, CFR_OPT_CAP, le, T.seer);
+  T.err |= le;
   int pid = g.gs_pid;
   const CfrEdge* E = T.edges + N.first_edge;
   double sum = 0.0;
-  for (int j = 0; j < s.n; j++) sum += E[T.optbuf[j].a].S[pid];
-  int j = np_choice(T.np, [&](int i) { return E[T.optbuf[i].a].S[pid] / sum; }, s.n, T.err);
+  for (int j = 0; j < nl; j++) sum += E[T.optbuf[j].a].S[pid];
+  int j = np_choice(T.np, [&](int i) { return E[T.optbuf[i].a].S[pid] / sum; }, nl, T.err);
   copy_row(T, row_of(T, root), reinterpret_cast<const uint32_t*>(&g));
   if (T.err || j < 0) return mk(O_NUM_NAMES, 0);
   return T.optbuf[j];

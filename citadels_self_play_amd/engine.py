@@ -18,6 +18,13 @@ from . import canon as _canon
 from . import layout as L
 
 
+NODE_DT = np.dtype([("parent", "<i4"), ("first_edge", "<i4"), ("n_children", "<i2"), ("edge_cap", "<i2"),
+                    ("depth", "<i2"), ("player", "i1"), ("gs_state", "i1"), ("flags", "u1"), ("winner", "i1"),
+                    ("pad", "u1", 6), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
+EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8", 6), ("S", "<f8", 6),
+                    ("CS", "<f8", 6)])
+
+
 def _ptr(t):
     return t.data_ptr()
 
@@ -89,6 +96,56 @@ class GameBatch:
                                                self.B, int(max_steps), int(g), _ptr(self.steps), _ptr(self.winner),
                                                _stream()), "cit_rollout_random")
         return self.steps, self.winner
+
+    # --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------------
+    def advance_random(self, lo, hi):
+        """The config-3 position harness: random.randint(lo, hi) random-policy steps per lane."""
+        steps = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_advance_random(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.seer),
+                                               self.B, int(lo), int(hi), _ptr(steps), _stream()),
+                   "cit_advance_random")
+        return steps
+
+    def seed_numpy(self, seeds=None):
+        """np.random.seed(s) per lane (numpy's legacy global stream used by the search)."""
+        d = self.device
+        seeds = self.seeds if seeds is None else torch.as_tensor(np.asarray(seeds, np.int64)).to(d)
+        self.np_mt = torch.zeros((L.MT_N, self.B), dtype=torch.int32, device=d)
+        self.np_idx = torch.zeros(self.B, dtype=torch.int32, device=d)
+        _lib.check(self.lib.cit_mt_seed(_ptr(self.np_mt), _ptr(self.np_idx), self.B, _ptr(seeds), 1, _stream()),
+                   "cit_mt_seed")
+
+    def cfr_decide(self, iters, node_cap=1024, edge_cap=None):
+        """run_mccfr(game, max_iterations=iters) (no model) on every lane; returns
+        (chosen [B,16] uint8 descriptors, stats [B,5] = root, nodes, edges, carry_outs, err)."""
+        if not hasattr(self, "np_mt"):
+            self.seed_numpy()
+        edge_cap = edge_cap or 8 * node_cap
+        per = self.lib.cit_cfr_pool_bytes(node_cap, edge_cap)
+        if per <= 0:
+            raise ValueError("node pool too large per tree")
+        need = per * self.B
+        if getattr(self, "pool", None) is None or self.pool.numel() < need:
+            self.pool = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self.optbuf = torch.empty((self.B, self.lib.cit_cfr_opt_cap(), 16), dtype=torch.uint8, device=self.device)
+        self.node_cap, self.edge_cap = node_cap, edge_cap
+        chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
+        stats = torch.zeros((self.B, 5), dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_cfr_decide(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt),
+                                           _ptr(self.np_idx), _ptr(self.seer), self.B, int(iters), _ptr(self.pool),
+                                           node_cap, edge_cap, _ptr(self.optbuf), _ptr(chosen), _ptr(stats),
+                                           _stream()), "cit_cfr_decide")
+        return chosen, stats
+
+    def tree(self, lane):
+        """(nodes, edges, rows) numpy views of one lane's search tree (host copy)."""
+        per = self.lib.cit_cfr_pool_bytes(self.node_cap, self.edge_cap)
+        base = self.pool[lane * per:(lane + 1) * per].cpu().numpy()
+        nc, ec = self.node_cap, self.edge_cap
+        nodes = base[:nc * 168].view(NODE_DT)
+        edges = base[nc * 168:nc * 168 + ec * 168].view(EDGE_DT)
+        rows = base[nc * 168 + ec * 168:].reshape(nc, L.GAME_BYTES)
+        return nodes, edges, rows
 
     # --- inspection --------------------------------------------------------------
     def rows(self):

@@ -97,6 +97,31 @@ int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitO
 int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
                        int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream);
 
+/* --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------ */
+
+/* Bytes of node pool per tree: node_cap CfrNode (168 B) + edge_cap CfrEdge
+ * (168 B) + node_cap packed game rows.  Opponent nodes reserve 10 edges. */
+int cit_cfr_pool_bytes(int node_cap, int edge_cap);
+int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */
+
+/* The config-3 position harness: k = random.randint(lo, hi) drawn from the
+ * lane's stream, then k random-policy steps (stops at a winner). */
+int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int lo, int hi,
+                       int32_t* steps, hipStream_t stream);
+
+/* run_mccfr(game, max_iterations=iters) without a model (run_utils.py:74-87):
+ * CFRNode(game) (deep_mccfr.py:8-49) + cfr_train(iters) (:187-205) +
+ * action_choice(live=True) (:67-91) for every lane, one tree per workgroup.
+ * The lane's games row becomes the root's game (the root's skip_false_choice
+ * mutates the game it is given, as in the reference); mt/mt_idx are the
+ * games' CPython stream, np_mt/np_idx numpy's global RandomState (seed them
+ * with cit_mt_seed(numpy_style=1)).  chosen[l] = the decision; stats[5*l..] =
+ * {root node, nodes, edges, carry_out calls, error bits}.  The tree stays in
+ * pool (B x cit_cfr_pool_bytes) for inspection / target extraction. */
+int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                   int B, int iters, void* pool, int node_cap, int edge_cap, CitOption* optbuf, CitOption* chosen,
+                   int32_t* stats, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,112 @@
+"""MCCFR on a real MI355X through the C ABI (cit_advance_random +
+cit_cfr_decide): the reference's MCCFR goldens (positions, node and
+carry_out counts, decisions, root arrays, RNG end states, whole trees), fresh
+seeds against the CFR oracle, and batch-size properties at config-3 scale.
+Same tolerance as the host test: exact except strategies (exp, rtol 1e-12)."""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from citadels_self_play_amd import canon
+from citadels_self_play_amd import layout as L
+from conftest import load_golden
+from test_cfr_host_golden import compare_node, dfs, hash_obj
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(seeds):
+    from citadels_self_play_amd.engine import GameBatch
+    return GameBatch(seeds, preset=True)
+
+
+def _run_golden(name):
+    recs = [r for r in load_golden(name) if not r.get("skip")]
+    b = _batch([r["seed"] for r in recs])
+    b.advance_random(0, 300)
+    rows = b.rows()
+    for l, r in enumerate(recs):
+        assert canon.canon_game(L.game_from_bytes(rows[l])) == r["position"], r["seed"]
+    b.seed_numpy()
+    chosen, stats = b.cfr_decide(recs[0]["iters"], node_cap=6144)
+    torch.cuda.synchronize()
+    chosen, stats, rows = chosen.cpu().numpy(), stats.cpu().numpy(), b.rows()
+    mt = b.mt.cpu().numpy().view(np.uint32)
+    idx = b.mt_idx.cpu().numpy()
+    npmt = b.np_mt.cpu().numpy().view(np.uint32)
+    npidx = b.np_idx.cpu().numpy()
+    for l, r in enumerate(recs):
+        root, n_nodes, n_edges, carry, err = stats[l]
+        assert err == 0, (r["seed"], err)
+        g = L.game_from_bytes(rows[l])
+        assert canon.canon_game(g) == r["root_game"], r["seed"]
+        assert n_nodes == r["nodes"], r["seed"]
+        assert carry == r["carry_outs"], r["seed"]
+        assert canon.canon_option(L.opt_from_bytes(chosen[l]), g) == r["chosen"], r["seed"]
+        nodes, edges, trows = b.tree(l)
+        compare_node(nodes, edges, trows, root, r["root"], (r["seed"], "root"))
+        assert hash_obj(mt[:, l].tolist() + [int(idx[l])]) == r["rng_after"][0], r["seed"]
+        assert hash_obj(npmt[:, l].tolist()) == r["rng_after"][1] and int(npidx[l]) == r["rng_after"][2]
+        if "tree" in r:
+            order = dfs(nodes, edges, root, [])
+            assert len(order) == len(r["tree"])
+            for k, (i, want) in enumerate(zip(order, r["tree"])):
+                compare_node(nodes, edges, trows, i, want, (r["seed"], k))
+
+
+def test_gpu_cfr_golden_200():
+    _run_golden("cfr_train200.json.gz")
+
+
+def test_gpu_cfr_golden_2000():
+    _run_golden("cfr_train2000.json.gz")
+
+
+def test_gpu_cfr_vs_oracle_fresh_seeds():
+    import cfr_oracle as CO
+    import citadels_oracle as O
+    seeds = list(range(5000, 5016))
+    b = _batch(seeds)
+    b.advance_random(0, 300)
+    b.seed_numpy()
+    chosen, stats = b.cfr_decide(200)
+    chosen, stats, rows = chosen.cpu().numpy(), stats.cpu().numpy(), b.rows()
+    for l, s in enumerate(seeds):
+        pos = CO.config3_position(s)
+        if pos is None:
+            assert L.game_from_bytes(rows[l]).terminal
+            continue
+        g, npr = pos
+        want, tr = CO.run_mccfr(g, npr, 200)
+        assert stats[l][4] == 0
+        gg = L.game_from_bytes(rows[l])
+        assert canon.canon_game(gg) == O.canon(tr.root.game), s
+        assert stats[l][1] == tr.count and stats[l][3] == tr.carry_outs, s
+        assert canon.canon_option(L.opt_from_bytes(chosen[l]), gg) == want.canon(), s
+
+
+def test_gpu_cfr_batch_properties():
+    """Config-3 scale (1024 decisions): no errors, deterministic, and a lane's
+    result does not depend on the batch it runs in."""
+    B = 1024
+    seeds = np.arange(9_000_000, 9_000_000 + B)
+    out = []
+    for rep in range(2):
+        b = _batch(seeds)
+        b.advance_random(0, 300)
+        b.seed_numpy()
+        chosen, stats = b.cfr_decide(200)
+        out.append((chosen.cpu().numpy(), stats.cpu().numpy(), b.rows()))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][2], out[1][2])
+    terminal = np.array([L.game_from_bytes(r).terminal for r in out[0][2]])
+    assert (out[0][1][~terminal, 4] == 0).all()
+    small = _batch(seeds[::97])
+    small.advance_random(0, 300)
+    small.seed_numpy()
+    c2, s2 = small.cfr_decide(200)
+    assert np.array_equal(c2.cpu().numpy(), out[0][0][::97])
+    assert np.array_equal(s2.cpu().numpy()[:, 1:], out[0][1][::97, 1:])

@@ -1,0 +1,50 @@
+"""Config 3 measurement: B preset positions (random.randint(0,300) random
+steps in), one no-model MCCFR decision (cfr_train(iters) + live choice) per
+position, all on one GPU.  Reports decisions/s and the carry_out transitions
+made inside the search per second (BASELINE.md config 3 unit)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from citadels_self_play_amd.engine import GameBatch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--node-cap", type=int, default=1024)
+    a = ap.parse_args()
+    for rep in range(a.reps):
+        s0 = 20_000_000 + rep * a.batch
+        b = GameBatch(np.arange(s0, s0 + a.batch), preset=True)
+        b.advance_random(0, 300)
+        b.seed_numpy()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        chosen, stats = b.cfr_decide(a.iters, node_cap=a.node_cap)
+        e1.record()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ms = e0.elapsed_time(e1)
+        st = stats.cpu().numpy()
+        ok = st[:, 4] == 0
+        print(json.dumps({"config": "config3", "B": a.batch, "iters": a.iters, "kernel_ms": ms, "wall_s": wall,
+                          "decisions_per_s": a.batch / (ms * 1e-3),
+                          "carry_out_per_s": float(st[:, 3].sum()) / (ms * 1e-3),
+                          "nodes_mean": float(st[:, 1].mean()), "nodes_max": int(st[:, 1].max()),
+                          "edges_max": int(st[:, 2].max()), "errors": int((~ok).sum()),
+                          "carry_outs": int(st[:, 3].sum())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,9 @@ _SIGS = {
     "cit_random_choice": ([vp, vp, vp, i32, vp, i32, vp, vp, vp, vp], i32),
     "cit_carry_out": ([vp, vp, vp, i32, vp, vp, vp], i32),
     "cit_rollout_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
+    "cit_encode_games": ([vp, i32, i32, vp, vp], i32),
+    "cit_encode_options": ([vp, vp, vp, i32, vp, vp], i32),
+    "cit_mlp_forward": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "cit_cfr_pool_bytes": ([i32, i32], i32),
     "cit_cfr_opt_cap": ([], i32),
     "cit_advance_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp], i32),

@@ -80,7 +80,7 @@ struct CfrTree {
 // inlining it at every call site of the search multiplies code size and
 // compile time.  The search reaches LDS rows through flat pointers here.
 #if defined(__HIPCC__)
-#define CIT_NOINLINE __host__ __device__ __attribute__((noinline))
+#define CIT_NOINLINE __host__ __device__ inline __attribute__((noinline))
 #else
 #define CIT_NOINLINE inline
 #endif
@@ -476,7 +476,7 @@ CIT_NOINLINE int cfr_choose(CfrTree& T, int n) {
     for (int i = 0; i < CIT_NP; i++) acc += E[a].CS[g.turn[i]] * (double)(CIT_NP - i);
     w[a] = acc / (double)hs;
   }
-  double s = np_sum([&w](int i) { return w[i]; }, nch, T.err);
+  double s = np_sum([&w](int i) { return w[i < CFR_ROLE_CHILDREN ? i : 0]; }, nch, T.err);
   if (s == 0.0) return np_choice_uniform(T.np, nch, T.err);
   return np_choice(T.np, [&w, s](int i) { return w[i] / s; }, nch, T.err);
 }
@@ -570,4 +570,110 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T, int root) {
   copy_row(T, row_of(T, root), reinterpret_cast<const uint32_t*>(&g));
   if (T.err || j < 0) return mk(O_NUM_NAMES, 0);
   return T.optbuf[j];
+}
+
+// ---------------------------------------------------------- cfr_pred (model)
+// Deep-MCCFR with value-net leaves (deep_mccfr.py:207-229), resumable: a tree
+// runs until a node deeper than max_depth needs its first leaf evaluation,
+// writes that node's encode_game row to `feat` and suspends (returns 1); the
+// caller evaluates every suspended tree's row in one batched MLP launch and
+// calls again with `probs`.  Only evaluations whose result the reference
+// uses are requested: pred_node_value is read only at depth > max_depth, and a
+// node's prediction never changes (model_inference on the same game), so it is
+// computed once per node (expand_role_pick's last inference: player 5).
+enum { CP_INIT = 0, CP_RUN = 1, CP_WAIT = 2, CP_DONE = 3 };
+struct CfrState {                       // 64 B, persists in HBM between launches
+  int32_t n_nodes, n_edges, err, carry_outs;
+  int32_t cur, it, phase, pending;
+  int32_t root, orig, pad[6];
+};
+static_assert(sizeof(CfrState) == 64, "CfrState layout");
+
+CIT_HD void cfr_state_load(CfrTree& T, const CfrState& S) {
+  T.n_nodes = S.n_nodes;
+  T.n_edges = S.n_edges;
+  T.err = (uint32_t)S.err;
+  T.carry_outs = (uint32_t)S.carry_outs;
+  T.orig = S.orig;
+}
+CIT_HD void cfr_state_save(const CfrTree& T, CfrState& S) {
+  S.n_nodes = T.n_nodes;
+  S.n_edges = T.n_edges;
+  S.err = (int32_t)T.err;
+  S.carry_outs = (int32_t)T.carry_outs;
+}
+
+CIT_NOINLINE void cfr_write_feat(CfrTree& T, int n, float* feat) {
+  const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
+  int pid = (T.nodes[n].flags & NF_ROLE_PICK) ? 5 : -1;
+  CFR_SYNC();
+  if (T.lane == 0) cit_encode_game(g, feat, pid);
+  CFR_SYNC();
+}
+
+// One resumption.  w0 must hold the lane's game when S.phase == CP_INIT.
+// Returns 1 when suspended for an evaluation, 0 when done (S.phase == CP_DONE).
+CIT_NOINLINE int cfr_pred_run(CfrTree& T, CfrState& S, int iters, int max_depth, const float* probs, float* feat,
+                              CitOpt& chosen) {
+  if (S.phase == CP_DONE) return 0;
+  if (S.phase == CP_INIT) {
+    S.orig = T.orig;
+    int root = cfr_node(T, *T.w0, -1, 0);
+    S.root = root;
+    S.it = 0;
+    if (root < 0 || T.err || (T.nodes[root].flags & NF_TERMINAL)) {
+      if (root >= 0 && !T.err) T.err |= CIT_ERR_VALUE;   // action_choice on a childless root raises
+      S.phase = CP_DONE;
+      chosen = mk(O_NUM_NAMES, 0);
+      return 0;
+    }
+    cfr_expand(T, root);
+    S.cur = root;
+    S.phase = CP_RUN;
+  } else if (S.phase == CP_WAIT) {
+    int n = S.pending;
+    CfrNode& N = T.nodes[n];
+    for (int k = 0; k < 6; k++) N.pred[k] = (double)(5.0f * probs[k]);   // model_reward_weights * wp (float32)
+    N.flags |= NF_PRED;
+    cfr_backprop(T, n, N.pred, true);
+    cfr_update_strategy(T, n);
+    S.cur = S.root;
+    S.it++;
+    S.phase = CP_RUN;
+  }
+  while (S.it < iters && !T.err) {
+    cfr_update_strategy(T, S.cur);
+    int a = cfr_choose(T, S.cur);
+    if (T.err) break;
+    int n = T.edges[T.nodes[S.cur].first_edge + a].child;
+    CfrNode& N = T.nodes[n];
+    if (N.depth > max_depth && !(N.flags & NF_TERMINAL)) {
+      cfr_expand(T, n);
+      if (T.err) break;
+      if (!(T.nodes[n].flags & NF_PRED)) {
+        cfr_write_feat(T, n, feat);
+        S.pending = n;
+        S.phase = CP_WAIT;
+        return 1;
+      }
+      cfr_backprop(T, n, T.nodes[n].pred, true);
+      cfr_update_strategy(T, n);
+      S.cur = S.root;
+    } else if (N.flags & NF_TERMINAL) {
+      double rw[6] = {0, 0, 0, 0, 0, 0};
+      if (N.winner >= 0) rw[N.winner] = 1.0;
+      cfr_backprop(T, n, rw, true);
+      cfr_update_strategy(T, n);
+      S.cur = S.root;
+    } else {
+      cfr_expand(T, n);
+      S.cur = n;
+    }
+    S.it++;
+  }
+  if (!T.err) cfr_update_strategy(T, S.root);
+  chosen = mk(O_NUM_NAMES, 0);
+  if (!T.err) chosen = cfr_live_choice(T, S.root);
+  S.phase = CP_DONE;
+  return 0;
 }

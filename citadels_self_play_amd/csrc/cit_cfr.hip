@@ -1,0 +1,97 @@
+// MCCFR kernel + C ABI (include/citadels.h, "MCCFR" section): one tree per
+// 64-lane workgroup; see cit_cfr.h for the search itself.
+#include <hip/hip_runtime.h>
+
+#include "../../include/citadels.h"
+#include "cit_cfr.h"
+
+#define ROW_W (CIT_GAME_BYTES / 4)
+
+namespace {
+
+__device__ __forceinline__ CitMT lane_mt(uint32_t* mt, const uint32_t* idx, int B, long l) {
+  CitMT r;
+  r.mt = mt + l;
+  r.stride = B;
+  r.pos = idx[l];
+  return r;
+}
+
+// One MCCFR decision per workgroup: a 64-lane team runs the search on its
+// tree (node pool in HBM, working rows in LDS).
+__global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
+                                                   uint32_t* npidx, uint64_t* seer, int B, int iters, uint8_t* pool,
+                                                   int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen,
+                                                   int32_t* stats) {
+  __shared__ __attribute__((aligned(16))) uint32_t w0s[ROW_W];
+  __shared__ __attribute__((aligned(16))) uint32_t w1s[ROW_W];
+  __shared__ __attribute__((aligned(16))) uint8_t tmps[128];
+  long l = blockIdx.x;
+  if (l >= B) return;
+  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
+  uint8_t* base = pool + per * l;
+  CfrTree T;
+  T.nodes = reinterpret_cast<CfrNode*>(base);
+  T.edges = reinterpret_cast<CfrEdge*>(base + (long)node_cap * sizeof(CfrNode));
+  T.rows = reinterpret_cast<uint32_t*>(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
+  T.node_cap = node_cap;
+  T.edge_cap = edge_cap;
+  T.n_nodes = T.n_edges = 0;
+  T.training = false;
+  T.py = lane_mt(mt, idx, B, l);
+  T.np = lane_mt(npmt, npidx, B, l);
+  T.seer = seer + l * CIT_SEER_MAX;
+  T.optbuf = optbuf + l * CFR_OPT_CAP;
+  T.w0 = reinterpret_cast<CitGame*>(w0s);
+  T.w1 = reinterpret_cast<CitGame*>(w1s);
+  T.tmp = tmps;
+  T.err = 0;
+  T.carry_outs = 0;
+  T.lane = threadIdx.x;
+  T.team = blockDim.x;
+  copy_row(T, w0s, games + l * ROW_W);
+  T.orig = T.w0->gs_pid;
+  int root = cfr_train(T, iters);
+  CitOpt c = mk(O_NUM_NAMES, 0);
+  if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
+  if (root >= 0) copy_row(T, games + l * ROW_W, row_of(T, root));
+  if (threadIdx.x == 0) {
+    chosen[l] = c;
+    idx[l] = T.py.pos;
+    npidx[l] = T.np.pos;
+    stats[5 * l + 0] = root;
+    stats[5 * l + 1] = T.n_nodes;
+    stats[5 * l + 2] = T.n_edges;
+    stats[5 * l + 3] = (int)T.carry_outs;
+    stats[5 * l + 4] = (int)T.err;
+  }
+}
+
+}  // namespace
+
+#define CHECK_LAUNCH()                       \
+  do {                                       \
+    hipError_t _e = hipGetLastError();       \
+    return _e == hipSuccess ? 0 : (int)_e;   \
+  } while (0)
+
+extern "C" {
+
+int cit_cfr_pool_bytes(int node_cap, int edge_cap) {
+  long b = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
+  return b > 0x7fffffff ? -1 : (int)b;
+}
+int cit_cfr_opt_cap(void) { return CFR_OPT_CAP; }
+
+int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                   int B, int iters, void* pool, int node_cap, int edge_cap, CitOption* optbuf, CitOption* chosen,
+                   int32_t* stats, hipStream_t stream) {
+  if (B <= 0 || iters < 0 || node_cap <= 0 || edge_cap <= 0 || !games || !mt || !mt_idx || !np_mt || !np_idx ||
+      !seer || !pool || !optbuf || !chosen || !stats)
+    return -1;
+  hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
+                     B, iters, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats);
+  CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -18,7 +18,7 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define CIT_HD __host__ __device__ __forceinline__
-#define CIT_HDI __host__ __device__
+#define CIT_HDI __host__ __device__ inline
 #else
 #define CIT_HD inline
 #define CIT_HDI inline

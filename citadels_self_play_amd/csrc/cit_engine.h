@@ -1576,6 +1576,91 @@ CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rn
   if (role_sample && g.gs_state != 0) refresh_used_roles(g);
 }
 
+// ============================================================ featurizers
+#define CIT_FEAT 418
+#define CIT_OPT_FEAT 131
+// Game.encode_game (game.py:91-128), written as 418 floats into `out`.
+// pid >= 0 replaces gamestate.player_id (expand_role_pick does that, :120-123).
+template <class F>
+CIT_HD void cit_encode_game(const CitGame& g, F* out, int pid = -1) {
+  for (int i = 0; i < CIT_FEAT; i++) out[i] = 0;
+  int cur = pid >= 0 ? pid : g.gs_pid;
+  for (int r = 0; r < 8; r++) out[r * 3 + g.roles[r] % 3] = 1;                 // [8,3] role variants
+  for (int p = 0; p < CIT_NP; p++) {                                              // [6,8] confirmed roles
+    int role = g.pl[p].role;
+    if (role >= 27) continue;
+    if (g.pl[cur].kr[p] & KR_CONFIRMED) out[24 + p * 8 + role / 3] = 1;
+  }
+  for (int p = 0; p < CIT_NP; p++) {
+    const CitPlayer& P = g.pl[p];
+    out[72 + p] = (F)count_points(P);                                             // points
+    out[78 + p] = (F)P.gold;                                                      // gold
+    out[84 + p] = (F)P.n_hand;                                                    // hand size
+    for (int i = 0; i < P.n_build; i++) {
+      out[90 + p * 40 + card_type(P.build[i])] += 1;                              // [6,40] built types
+      out[330 + p * 5 + card_suit(P.build[i])] += 1;                              // [6,5] built suits
+    }
+  }
+  out[360 + cur] = 1;                                                             // current player
+  out[366 + g.gs_state] = 1;                                                      // state one-hot [11]
+  out[377] = g.ending ? 1 : 0;
+  for (int r = 0; r < 8; r++) {                                                   // [8,5] role properties
+    uint8_t v = g.rp[r];
+    out[378 + r * 5 + 0] = (v & RP_DEAD) ? 1 : 0;
+    out[378 + r * 5 + 1] = rp_warrant(v) ? 1 : 0;
+    out[378 + r * 5 + 2] = (v & RP_POSSESSED) ? 1 : 0;
+    out[378 + r * 5 + 3] = (v & RP_ROBBED) ? 1 : 0;
+    out[378 + r * 5 + 4] = rp_blackmail(v) ? 1 : 0;
+  }
+}
+
+// option.encode_option (option.py:52-115) for descriptor `o` generated on `g`
+// (hand-slot masks resolve against g).  Only the first matching branch of the
+// reference's elif chain writes: a tuple choice, an int role choice, `cards`,
+// `card_handouts` and next_gamestate encode nothing beyond name + perpetrator.
+template <class F>
+CIT_HD void cit_encode_option(const CitOpt& o, const CitGame& g, F* out) {
+  for (int i = 0; i < CIT_OPT_FEAT; i++) out[i] = 0;
+  out[o.name] = 1;
+  out[47 + o.perp] = 1;
+  switch (o.name) {
+    case O_REVEAL_BLACKMAIL: case O_REVEAL_WARRANT: case O_WEAPON_STORAGE: case O_SPY: case O_MAGIC_HAND_CHANGE:
+    case O_LOOK_AT_HAND: case O_TAKE_FROM_HAND: case O_GIVE_CROWN: case O_CARDINAL: case O_WARLORD: case O_MARSHAL:
+    case O_DIPLOMAT:
+      out[53 + o.target] = 1;
+      break;
+    case O_ROLE_PICK:
+      out[60 + o.a] = 1;
+      break;
+    case O_GOLD_OR_CARD:
+      out[76 + o.a] = 1;                       // gold 0, card 1
+      break;
+    case O_BLACKMAIL_RESPONSE:
+      out[76 + 2 + o.a] = 1;                   // pay 2, not_pay 3
+      break;
+    case O_NAVIGATOR:
+      out[76 + 6 + o.a] = 1;                   // 4gold 6, 4card 7
+      break;
+    case O_MAGIC_SCHOOL:
+      out[76 + 8 + o.a] = 1;                   // trade..unique 8..12
+      break;
+    case O_LAB: case O_LIGHTHOUSE: case O_MUSEUM: case O_SCHOLAR_PICK: case O_BUILD:
+      out[89 + card_type(o.a)] = 1;
+      break;
+    case O_WHICH_CARD:
+      if (!(o.flags & OF_TUPLE)) out[89 + card_type(o.a)] = 1;   // [card]; a tuple matches no branch
+      break;
+    case O_MAGISTRATE_WARRANT: case O_BLACKMAIL:
+      out[60 + o.a] = 1;                       // real_target
+      break;
+    case O_ABBOT_GOLD_OR_CARD:
+      out[130] = (F)o.b;                       // number of "card"
+      break;
+    default:
+      break;
+  }
+}
+
 // One random-policy step (compare_to_random.py:37-39): get_options ->
 // random.choice -> carry_out.  Returns 1 when the lane is done (winner or error).
 CIT_HD int cit_random_step(CitGame& g, CitMT& rng, uint64_t* seer) {

@@ -192,4 +192,66 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
   free(w1);
 }
 
+void cith_encode_games(const CitGame* g, int B, int pid, float* out) {
+  for (int l = 0; l < B; l++) cit_encode_game(g[l], out + (long)l * CIT_FEAT, pid);
+}
+void cith_encode_options(const CitGame* g, const CitOpt* opts, int n, float* out) {
+  for (int i = 0; i < n; i++) cit_encode_option(opts[i], *g, out + (long)i * CIT_OPT_FEAT);
+}
+
+// One resumption of cfr_pred for every lane (see cfr_pred_run); returns the
+// number of lanes now waiting for an evaluation (features in feat[l]).
+int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx, uint64_t* seer,
+                       int B, int iters, int max_depth, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
+                       CfrState* st, const float* probs, float* feat, CitOpt* chosen) {
+  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
+  CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
+  CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
+  uint8_t tmp[128];
+  int waiting = 0;
+  for (int l = 0; l < B; l++) {
+    CfrState& S = st[l];
+    if (S.phase == CP_DONE) continue;
+    uint8_t* base = pool + per * l;
+    CfrTree T;
+    T.nodes = (CfrNode*)base;
+    T.edges = (CfrEdge*)(base + (long)node_cap * sizeof(CfrNode));
+    T.rows = (uint32_t*)(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
+    T.node_cap = node_cap;
+    T.edge_cap = edge_cap;
+    T.training = false;
+    T.py = lane_rng(mt, idx, B, l);
+    T.np = lane_rng(npmt, npidx, B, l);
+    T.seer = seer + (long)l * CIT_SEER_MAX;
+    T.optbuf = optbuf + (long)l * CFR_OPT_CAP;
+    T.w0 = w0;
+    T.w1 = w1;
+    T.tmp = tmp;
+    T.lane = 0;
+    T.team = 1;
+    if (S.phase == CP_INIT) {
+      T.n_nodes = T.n_edges = 0;
+      T.err = 0;
+      T.carry_outs = 0;
+      T.orig = g[l].gs_pid;
+      memcpy(w0, &g[l], CIT_GAME_BYTES);
+    } else {
+      cfr_state_load(T, S);
+    }
+    CitOpt c;
+    int r = cfr_pred_run(T, S, iters, max_depth, probs + 6L * l, feat + (long)CIT_FEAT * l, c);
+    cfr_state_save(T, S);
+    waiting += r;
+    if (!r) {
+      chosen[l] = c;
+      if (S.root >= 0) memcpy(&g[l], row_of(T, S.root), CIT_GAME_BYTES);
+    }
+    idx[l] = T.py.pos;
+    npidx[l] = T.np.pos;
+  }
+  free(w0);
+  free(w1);
+  return waiting;
+}
+
 }  // extern "C"

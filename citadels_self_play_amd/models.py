@@ -1,0 +1,77 @@
+"""The value network of the reference (algorithms/models.py:4-24):
+ValueOnlyNN(418, hidden) = fc1 -> BN -> ReLU -> Dropout(0.2) -> fc2 -> BN ->
+ReLU -> Dropout -> fc3 -> ReLU -> fc4 (6 logits).  Same parameter names, so a
+reference state_dict loads unchanged.  `ValueNet` is its inference form on
+the MI355X: BatchNorm folded into fc1/fc2 (eval mode), weights transposed to
+[in][out] and resident in HBM, forward = the fp32-MFMA kernel cit_mlp_forward
+(+ square_and_normalize, train_utils.py:143-145)."""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+FEAT = 418
+
+
+class ValueOnlyNN(nn.Module):
+    def __init__(self, input_size=FEAT, hidden_size=512):
+        super().__init__()
+        self.fc1 = nn.Linear(input_size, hidden_size)
+        self.bn1 = nn.BatchNorm1d(hidden_size)
+        self.dropout1 = nn.Dropout(0.2)
+        self.fc2 = nn.Linear(hidden_size, hidden_size // 2)
+        self.bn2 = nn.BatchNorm1d(hidden_size // 2)
+        self.dropout2 = nn.Dropout(0.2)
+        self.fc3 = nn.Linear(hidden_size // 2, hidden_size // 4)
+        self.fc4 = nn.Linear(hidden_size // 4, 6)
+
+    def forward(self, x):
+        x = self.dropout1(F.relu(self.bn1(self.fc1(x))))
+        x = self.dropout2(F.relu(self.bn2(self.fc2(x))))
+        return self.fc4(F.relu(self.fc3(x)))
+
+
+def square_and_normalize(x, dim=-1):
+    sq = torch.pow(x, 2)
+    return sq / sq.sum(dim=dim, keepdim=True)
+
+
+def fold(model):
+    """Eval-mode BatchNorm folded into the preceding Linear, weights as [in][out]
+    fp32 (CPU tensors): w1t, b1, w2t, b2, w3t, b3, w4t, b4."""
+    m = model.eval()
+    with torch.no_grad():
+        out = []
+        for fc, bn in ((m.fc1, m.bn1), (m.fc2, m.bn2), (m.fc3, None), (m.fc4, None)):
+            w = fc.weight.detach().float().cpu()
+            b = fc.bias.detach().float().cpu()
+            if bn is not None:
+                s = bn.weight.detach().float().cpu() / torch.sqrt(bn.running_var.detach().float().cpu() + bn.eps)
+                w = w * s[:, None]
+                b = (b - bn.running_mean.detach().float().cpu()) * s + bn.bias.detach().float().cpu()
+            out += [w.t().contiguous(), b.contiguous()]
+    return out
+
+
+class ValueNet:
+    """Device-resident folded weights + the MFMA forward."""
+
+    def __init__(self, model, device="cuda"):
+        if model.fc1.out_features != 512:
+            raise ValueError("the MFMA kernel is built for ValueOnlyNN(418, 512)")
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        self.host = fold(model)
+        self.w = [t.to(self.device) for t in self.host]
+
+    def forward(self, feat, logits=False):
+        feat = feat.contiguous()
+        M = feat.shape[0]
+        probs = torch.empty((M, 6), dtype=torch.float32, device=self.device)
+        lg = torch.empty((M, 6), dtype=torch.float32, device=self.device) if logits else None
+        ptrs = [t.data_ptr() for t in self.w]
+        _lib.check(self.lib.cit_mlp_forward(feat.data_ptr(), M, *ptrs, probs.data_ptr(),
+                                            lg.data_ptr() if lg is not None else None,
+                                            torch.cuda.current_stream().cuda_stream), "cit_mlp_forward")
+        return (probs, lg) if logits else probs

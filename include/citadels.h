@@ -97,6 +97,25 @@ int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitO
 int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
                        int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream);
 
+/* --- featurizers and the value MLP ---------------------------------------- */
+
+/* Game.encode_game() (game/game.py:91-128) for every lane: feat[B][418] fp32.
+ * pid >= 0 encodes as if gamestate.player_id == pid (deep_mccfr.py:120-123). */
+int cit_encode_games(const void* games, int B, int pid, float* feat, hipStream_t stream);
+/* option.encode_option() (game/option.py:52-115): out[n][131] fp32 for
+ * descriptor opts[i] generated on game lane_of[i]. */
+int cit_encode_options(const void* games, const CitOption* opts, const int32_t* lane_of, int n, float* out,
+                       hipStream_t stream);
+/* ValueOnlyNN(418, 512) eval forward + square_and_normalize
+ * (algorithms/models.py:17-24, train_utils.py:143-145): probs[M][6] (and
+ * logits[M][6] if non-null).  BatchNorm folded into fc1/fc2 by the caller;
+ * weights transposed to [in][out] (w1t [418][512], w2t [512][256],
+ * w3t [256][128], w4t [128][6]).  fp32 MFMA, each output a k-ordered fmaf
+ * chain from 0, then + bias. */
+int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1, const float* w2t, const float* b2,
+                    const float* w3t, const float* b3, const float* w4t, const float* b4, float* probs, float* logits,
+                    hipStream_t stream);
+
 /* --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------ */
 
 /* Bytes of node pool per tree: node_cap CfrNode (168 B) + edge_cap CfrEdge

@@ -337,7 +337,8 @@ class Tree:
         return g.carry_out(o)
 
     def infer(self, g):
-        return self.model(g)
+        """model_inference (deep_mccfr.py:364-374): float32 winning probabilities."""
+        return np.asarray(self.model(g), np.float32)
 
     def cfr_train(self, iters):
         """:187-205"""

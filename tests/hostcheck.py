@@ -17,11 +17,11 @@ _lib = None
 
 
 def build(force=False):
-    srcs = [os.path.join(SRC, f) for f in ("cit_host.cpp", "cit_engine.h", "cit_core.h")]
+    srcs = [os.path.join(SRC, f) for f in ("cit_host.cpp", "cit_engine.h", "cit_core.h", "cit_cfr.h")]
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(s) for s in srcs):
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", srcs[0], "-o", LIB])
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", srcs[0], "-o", LIB])
     return LIB
 
 
@@ -127,3 +127,41 @@ class HostCfr:
         edges = base[self.node_cap * 168:self.node_cap * 168 + self.edge_cap * 168].view(EDGE_DT)
         rows = base[self.node_cap * 168 + self.edge_cap * 168:].reshape(self.node_cap, L.GAME_BYTES)
         return nodes, edges, rows
+
+
+def encode_games(hb, pid=-1):
+    out = np.zeros((hb.B, 418), np.float32)
+    lib().cith_encode_games(_p(hb.games), C.c_int(hb.B), C.c_int(pid), _p(out))
+    return out
+
+
+def encode_options(game_row, opts):
+    opts = np.ascontiguousarray(opts, np.uint8)
+    out = np.zeros((len(opts), 131), np.float32)
+    row = np.ascontiguousarray(game_row, np.uint8)
+    lib().cith_encode_options(_p(row), _p(opts), C.c_int(len(opts)), _p(out))
+    return out
+
+
+def cfr_pred(cf, iters, max_depth, mlp):
+    """Drive the resumable host-build cfr_pred: between resumptions, evaluate
+    the suspended lanes' feature rows with `mlp` (feat [k,418] -> probs [k,6])."""
+    hb = cf.hb
+    B = hb.B
+    st = np.zeros((B, 16), np.int32)            # CfrState (64 B)
+    probs = np.zeros((B, 6), np.float32)
+    feat = np.zeros((B, 418), np.float32)
+    chosen = np.zeros((B, 16), np.uint8)
+    rounds = 0
+    while True:
+        w = lib().cith_cfr_pred_step(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(cf.npmt), _p(cf.npidx), _p(hb.seer),
+                                     C.c_int(B), C.c_int(iters), C.c_int(max_depth), _p(cf.pool),
+                                     C.c_int(cf.node_cap), C.c_int(cf.edge_cap), _p(cf.optbuf), _p(st), _p(probs),
+                                     _p(feat), _p(chosen))
+        if w == 0:
+            break
+        waiting = st[:, 6] == 2
+        probs[waiting] = mlp(feat[waiting])
+        rounds += 1
+    stats = np.stack([st[:, 8], st[:, 0], st[:, 1], st[:, 3], st[:, 2]], axis=1)
+    return chosen, stats, rounds

@@ -38,7 +38,10 @@ def arr(x):
 
 
 def node_rec(n):
-    return {
+    extra = {}
+    if hasattr(n, "pred_node_value"):
+        extra["pred"] = arr(n.pred_node_value)
+    return {**extra,
         "depth": n.depth, "player": n.current_player_id, "role_pick": int(bool(n.role_pick_node)),
         "terminal": int(bool(n.game.terminal)), "n_children": len(n.children),
         "node_value": arr(n.node_value), "wp": arr(n.winning_probabilities),
@@ -58,7 +61,25 @@ def count_nodes(n):
     return 1 + sum(count_nodes(c) for _, c in n.children)
 
 
-def case(seed, iters, tree):
+def seeded_model():
+    """ValueOnlyNN(418, 512): torch.manual_seed(0) init + the seeded BatchNorm
+    statistics of tools/gen_golden_mlp.py ("bn" variant), eval mode."""
+    import torch
+    from algorithms.models import ValueOnlyNN
+    torch.manual_seed(0)
+    m = ValueOnlyNN(418, hidden_size=512)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for bn in (m.bn1, m.bn2):
+            n = bn.num_features
+            bn.running_mean.copy_(torch.randn(n, generator=g) * 0.5)
+            bn.running_var.copy_(torch.rand(n, generator=g) * 2 + 0.1)
+            bn.weight.copy_(torch.rand(n, generator=g) + 0.5)
+            bn.bias.copy_(torch.randn(n, generator=g) * 0.1)
+    return m.eval()
+
+
+def case(seed, iters, tree, model=None):
     import game.option as gopt
     from run_utils import create_game, run_mccfr
     random.seed(seed)
@@ -83,7 +104,13 @@ def case(seed, iters, tree):
     gopt.option.carry_out = counting
     t = time.time()
     try:
-        chosen, root = run_mccfr(g, max_iterations=iters)
+        if model is None:
+            chosen, root = run_mccfr(g, max_iterations=iters)
+        else:   # run_mccfr's model branch (run_utils.py:78-81) on the CPU
+            from algorithms.deep_mccfr import CFRNode
+            root = CFRNode(g, original_player_id=g.gamestate.player_id, model=model, training=False, device="cpu")
+            root.cfr_pred(max_iterations=iters, max_depth=10)
+            _, chosen = root.action_choice(live=True)
         rec["error"] = None
     except Exception as e:
         rec["error"] = type(e).__name__
@@ -106,7 +133,20 @@ def case(seed, iters, tree):
     return rec
 
 
-if __name__ == "__main__":
+def main_pred():
+    model = seeded_model()
+    recs = []
+    t = time.time()
+    for s in range(16):
+        recs.append(case(s, 200, tree=s < 4, model=model))
+        print("pred", s, recs[-1].get("nodes"), recs[-1].get("carry_outs"), "%.1fs" % (time.time() - t), flush=True)
+    with gzip.open(os.path.join(OUT, "cfr_pred200.json.gz"), "wt") as f:
+        json.dump(recs, f, separators=(",", ":"))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "pred":
+    main_pred()
+elif __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     recs = []
     t = time.time()

@@ -35,6 +35,8 @@ _SIGS = {
     "cit_cfr_opt_cap": ([], i32),
     "cit_advance_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp], i32),
     "cit_cfr_decide": ([vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, vp], i32),
+    "cit_cfr_state_bytes": ([], i32),
+    "cit_cfr_pred_step": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp], i32),
 }
 
 

@@ -67,6 +67,60 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   }
 }
 
+// One resumption of cfr_pred (cit_cfr.h: cfr_pred_run) per tree; lane 0 adds
+// 1 to *waiting when the tree suspends for a leaf evaluation.
+__global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
+                                                      uint32_t* npidx, uint64_t* seer, int B, int iters, int max_depth,
+                                                      uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
+                                                      CfrState* state, const float* probs, float* feat,
+                                                      CitOpt* chosen, int32_t* waiting) {
+  __shared__ __attribute__((aligned(16))) uint32_t w0s[ROW_W];
+  __shared__ __attribute__((aligned(16))) uint32_t w1s[ROW_W];
+  __shared__ __attribute__((aligned(16))) uint8_t tmps[128];
+  long l = blockIdx.x;
+  if (l >= B) return;
+  CfrState S = state[l];
+  if (S.phase == CP_DONE) return;
+  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
+  uint8_t* base = pool + per * l;
+  CfrTree T;
+  T.nodes = reinterpret_cast<CfrNode*>(base);
+  T.edges = reinterpret_cast<CfrEdge*>(base + (long)node_cap * sizeof(CfrNode));
+  T.rows = reinterpret_cast<uint32_t*>(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
+  T.node_cap = node_cap;
+  T.edge_cap = edge_cap;
+  T.training = false;
+  T.py = lane_mt(mt, idx, B, l);
+  T.np = lane_mt(npmt, npidx, B, l);
+  T.seer = seer + l * CIT_SEER_MAX;
+  T.optbuf = optbuf + l * CFR_OPT_CAP;
+  T.w0 = reinterpret_cast<CitGame*>(w0s);
+  T.w1 = reinterpret_cast<CitGame*>(w1s);
+  T.tmp = tmps;
+  T.lane = threadIdx.x;
+  T.team = blockDim.x;
+  if (S.phase == CP_INIT) {
+    T.n_nodes = T.n_edges = 0;
+    T.err = 0;
+    T.carry_outs = 0;
+    copy_row(T, w0s, games + l * ROW_W);
+    T.orig = T.w0->gs_pid;
+  } else {
+    cfr_state_load(T, S);
+  }
+  CitOpt c;
+  int r = cfr_pred_run(T, S, iters, max_depth, probs + 6 * l, feat + (long)CIT_FEAT * l, c);
+  cfr_state_save(T, S);
+  if (!r && S.root >= 0) copy_row(T, games + l * ROW_W, row_of(T, S.root));
+  if (threadIdx.x == 0) {
+    state[l] = S;
+    if (!r) chosen[l] = c;
+    idx[l] = T.py.pos;
+    npidx[l] = T.np.pos;
+    if (r) atomicAdd(waiting, 1);
+  }
+}
+
 }  // namespace
 
 #define CHECK_LAUNCH()                       \
@@ -91,6 +145,21 @@ int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt,
     return -1;
   hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
                      B, iters, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats);
+  CHECK_LAUNCH();
+}
+
+int cit_cfr_state_bytes(void) { return (int)sizeof(CfrState); }
+
+int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                      int B, int iters, int max_depth, void* pool, int node_cap, int edge_cap, CitOption* optbuf,
+                      void* state, const float* probs, float* feat, CitOption* chosen, int32_t* waiting,
+                      hipStream_t stream) {
+  if (B <= 0 || iters < 0 || node_cap <= 0 || edge_cap <= 0 || !games || !mt || !mt_idx || !np_mt || !np_idx ||
+      !seer || !pool || !optbuf || !state || !probs || !feat || !chosen || !waiting)
+    return -1;
+  hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
+                     seer, B, iters, max_depth, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
+                     (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting);
   CHECK_LAUNCH();
 }
 

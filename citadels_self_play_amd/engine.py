@@ -120,6 +120,17 @@ class GameBatch:
         (chosen [B,16] uint8 descriptors, stats [B,5] = root, nodes, edges, carry_outs, err)."""
         if not hasattr(self, "np_mt"):
             self.seed_numpy()
+        self._pool(node_cap, edge_cap)
+        node_cap, edge_cap = self.node_cap, self.edge_cap
+        chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
+        stats = torch.zeros((self.B, 5), dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_cfr_decide(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt),
+                                           _ptr(self.np_idx), _ptr(self.seer), self.B, int(iters), _ptr(self.pool),
+                                           node_cap, edge_cap, _ptr(self.optbuf), _ptr(chosen), _ptr(stats),
+                                           _stream()), "cit_cfr_decide")
+        return chosen, stats
+
+    def _pool(self, node_cap, edge_cap):
         edge_cap = edge_cap or 8 * node_cap
         per = self.lib.cit_cfr_pool_bytes(node_cap, edge_cap)
         if per <= 0:
@@ -129,13 +140,38 @@ class GameBatch:
             self.pool = torch.empty(need, dtype=torch.uint8, device=self.device)
             self.optbuf = torch.empty((self.B, self.lib.cit_cfr_opt_cap(), 16), dtype=torch.uint8, device=self.device)
         self.node_cap, self.edge_cap = node_cap, edge_cap
-        chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
-        stats = torch.zeros((self.B, 5), dtype=torch.int32, device=self.device)
-        _lib.check(self.lib.cit_cfr_decide(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt),
-                                           _ptr(self.np_idx), _ptr(self.seer), self.B, int(iters), _ptr(self.pool),
-                                           node_cap, edge_cap, _ptr(self.optbuf), _ptr(chosen), _ptr(stats),
-                                           _stream()), "cit_cfr_decide")
-        return chosen, stats
+
+    def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000):
+        """run_mccfr(game, model, max_iterations=iters) with a model and training=False
+        (cfr_pred(iters, max_depth) + live action choice) on every lane.  `net` is a
+        models.ValueNet; leaf rows of all suspended trees are evaluated in one MFMA
+        launch per round.  Returns (chosen, stats [B,5], rounds)."""
+        if not hasattr(self, "np_mt"):
+            self.seed_numpy()
+        self._pool(node_cap, edge_cap)
+        d = self.device
+        state = torch.zeros((self.B, self.lib.cit_cfr_state_bytes() // 4), dtype=torch.int32, device=d)
+        feat = torch.zeros((self.B, 418), dtype=torch.float32, device=d)
+        probs = torch.zeros((self.B, 6), dtype=torch.float32, device=d)
+        chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=d)
+        waiting = torch.zeros(1, dtype=torch.int32, device=d)
+        w = [t.data_ptr() for t in net.w]
+        rounds = 0
+        while rounds < max_rounds:
+            waiting.zero_()
+            _lib.check(self.lib.cit_cfr_pred_step(
+                _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
+                _ptr(self.seer), self.B, int(iters), int(max_depth), _ptr(self.pool), self.node_cap, self.edge_cap,
+                _ptr(self.optbuf), _ptr(state), _ptr(probs), _ptr(feat), _ptr(chosen), _ptr(waiting), _stream()),
+                "cit_cfr_pred_step")
+            if int(waiting.item()) == 0:
+                break
+            _lib.check(self.lib.cit_mlp_forward(_ptr(feat), self.B, *w, _ptr(probs), None, _stream()),
+                       "cit_mlp_forward")
+            rounds += 1
+        st = state.cpu()
+        stats = torch.stack([st[:, 8], st[:, 0], st[:, 1], st[:, 3], st[:, 2]], dim=1)
+        return chosen, stats, rounds
 
     def tree(self, lane):
         """(nodes, edges, rows) numpy views of one lane's search tree (host copy)."""

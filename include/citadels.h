@@ -141,6 +141,21 @@ int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt,
                    int B, int iters, void* pool, int node_cap, int edge_cap, CitOption* optbuf, CitOption* chosen,
                    int32_t* stats, hipStream_t stream);
 
+/* Deep MCCFR with value-net leaves: cfr_pred(iters, max_depth)
+ * (deep_mccfr.py:207-229) as run_mccfr runs it with a model and training=False
+ * (run_utils.py:78-81), resumable.  Zero `state` (B x cit_cfr_state_bytes())
+ * before the first call.  Each call advances every unfinished tree until it
+ * needs its next leaf evaluation (that node's encode_game row goes to
+ * feat[l][418] and *waiting is incremented) or finishes (chosen[l], games[l] =
+ * root game).  Between calls evaluate feat with cit_mlp_forward into
+ * probs[l][6]; stop when a call leaves *waiting == 0.  Leaves are evaluated
+ * once per node (the reference recomputes the same value). */
+int cit_cfr_state_bytes(void);
+int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                      int B, int iters, int max_depth, void* pool, int node_cap, int edge_cap, CitOption* optbuf,
+                      void* state, const float* probs, float* feat, CitOption* chosen, int32_t* waiting,
+                      hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

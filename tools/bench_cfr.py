@@ -35,6 +35,7 @@ def main():
         b = GameBatch(np.arange(s0, s0 + a.batch), preset=True)
         b.advance_random(0, 300)
         b.seed_numpy()
+        term0 = b.terminal().cpu().numpy()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
@@ -54,7 +55,9 @@ def main():
                           "decisions_per_s": a.batch / (ms * 1e-3),
                           "carry_out_per_s": float(st[:, 3].sum()) / (ms * 1e-3),
                           "nodes_mean": float(st[:, 1].mean()), "nodes_max": int(st[:, 1].max()),
-                          "edges_max": int(st[:, 2].max()), "errors": int((~ok).sum()),
+                          "edges_max": int(st[:, 2].max()), "terminal_positions": int(term0.sum()),
+                          "errors_nonterminal": int((~ok & ~term0).sum()),
+                          "err_bits": int(np.bitwise_or.reduce(st[~term0, 4])) if (~term0).any() else 0,
                           "carry_outs": int(st[:, 3].sum())}), flush=True)
 
 

@@ -677,3 +677,94 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T, CfrState& S, int iters, int max_depth,
   S.phase = CP_DONE;
   return 0;
 }
+
+// ----------------------------------------------------- training targets
+// get_all_targets (deep_mccfr.py:258-274) + build_train_targets (:321-345)
+// over a finished tree, pre-order.  build_train_targets is always called with
+// its default threshold (get_all_targets never passes its own, :268).
+#define CFR_TARGET_THRESHOLD 15.0
+
+CIT_HD bool cfr_is_target(const CfrTree& T, int n) {
+  const CfrNode& N = T.nodes[n];
+  if (N.n_children <= 0) return false;
+  double s = 0.0;
+  for (int k = 0; k < 6; k++) s += N.nv[k];     // integer-valued: order-free
+  return s >= CFR_TARGET_THRESHOLD;
+}
+
+// Pre-order successor through parent links (-1 after the last node).
+CIT_HD int cfr_preorder_next(const CfrTree& T, int n) {
+  const CfrNode& N = T.nodes[n];
+  if (N.n_children > 0) return T.edges[N.first_edge].child;
+  for (;;) {
+    int p = T.nodes[n].parent;
+    if (p < 0) return -1;
+    const CfrNode& P = T.nodes[p];
+    int j = 0;
+    while (j < P.n_children && T.edges[P.first_edge + j].child != n) j++;
+    if (j + 1 < P.n_children) return T.edges[P.first_edge + j + 1].child;
+    n = p;
+  }
+}
+
+// The tree of lane l in a node pool (nodes | edges | rows per tree), read-only use.
+CIT_HD CfrTree cfr_tree_view(uint8_t* pool, long l, int node_cap, int edge_cap) {
+  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
+  uint8_t* base = pool + per * l;
+  CfrTree T;
+  T.nodes = reinterpret_cast<CfrNode*>(base);
+  T.edges = reinterpret_cast<CfrEdge*>(base + (long)node_cap * sizeof(CfrNode));
+  T.rows = reinterpret_cast<uint32_t*>(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
+  T.node_cap = node_cap;
+  T.edge_cap = edge_cap;
+  return T;
+}
+
+// Number of targets and of their children (option rows).
+CIT_HD void cfr_count_targets(const CfrTree& T, int root, int32_t& n_targets, int32_t& n_children) {
+  n_targets = n_children = 0;
+  if (root < 0) return;
+  for (int n = root; n >= 0; n = cfr_preorder_next(T, n))
+    if (cfr_is_target(T, n)) {
+      n_targets++;
+      n_children += T.nodes[n].n_children;
+    }
+}
+
+// Emit the targets from offsets (t0 targets, c0 children).  Per target k:
+//   meta[k] = {lane, node, player (-1: the game's own), n_children, first child row}
+//   feat[k][418] = encode_game (role-pick node: player randint(0, 5) of the tree's stream)
+//   value[k][6] = node_value;  regret rows dist[c0 + j] (role-pick: cumulative_regrets[i]),
+//   all ones when they sum to 0;  opt_feat[c0 + j][131] = encode_option of child j.
+CIT_HD void cfr_emit_targets(const CfrTree& T, CitMT& py, int root, int lane, int32_t t0, int32_t c0, int32_t* meta,
+                             float* feat, double* value, double* dist, float* opt_feat) {
+  if (root < 0) return;
+  int32_t t = t0, c = c0;
+  for (int n = root; n >= 0; n = cfr_preorder_next(T, n)) {
+    if (!cfr_is_target(T, n)) continue;
+    const CfrNode& N = T.nodes[n];
+    const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
+    const CfrEdge* E = T.edges + N.first_edge;
+    int pid = -1, row = 0;
+    if (N.flags & NF_ROLE_PICK) {
+      pid = (int)mt_randbelow(py, 6u);
+      row = pid;
+    }
+    int32_t* m = meta + 5 * (long)t;
+    m[0] = lane;
+    m[1] = n;
+    m[2] = pid;
+    m[3] = N.n_children;
+    m[4] = c;
+    cit_encode_game(g, feat + (long)t * CIT_FEAT, pid);
+    for (int k = 0; k < 6; k++) value[(long)t * 6 + k] = N.nv[k];
+    bool zero = true;
+    for (int j = 0; j < N.n_children; j++) zero = zero && E[j].R[row] == 0.0;
+    for (int j = 0; j < N.n_children; j++) {
+      dist[c + j] = zero ? 1.0 : E[j].R[row];
+      cit_encode_option(E[j].opt, g, opt_feat + (long)(c + j) * CIT_OPT_FEAT);
+    }
+    c += N.n_children;
+    t++;
+  }
+}

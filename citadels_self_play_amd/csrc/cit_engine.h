@@ -1674,3 +1674,32 @@ CIT_HD int cit_random_step(CitGame& g, CitMT& rng, uint64_t* seer) {
   int w = cit_carry_out(g, o, rng);
   return (w >= 0 || g.err || g.terminal) ? 1 : 0;
 }
+
+// create_a_random_game(max_move) (run_utils.py:55-73) on a lane whose CPython
+// stream is already seeded: k = randint(1, max_move); create_game(); a random
+// playout to the winner keeping the game after every step (deepcopy ->
+// `ring`, the last max_move snapshots, CIT_GAME_BYTES each); the result is
+// games[-k] while the stream stays where the playout left it.  Returns the
+// number of steps into the game of the returned position (-1 on error:
+// games[-k] past the front raises IndexError in the reference).
+CIT_HD int cit_random_position(CitGame& g, CitMT& rng, uint64_t* seer, uint32_t* ring, int max_move) {
+  const int W = CIT_GAME_BYTES / 4;
+  int k = 1 + (int)mt_randbelow(rng, (uint32_t)max_move);
+  cit_init_game(g, rng, true);
+  uint32_t* gw = reinterpret_cast<uint32_t*>(&g);
+  int n = 0;                                   // snapshots taken
+  for (int i = 0; i < W; i++) ring[i] = gw[i];
+  n = 1;
+  while (!g.terminal && !g.err) {
+    if (n > CIT_ROLLOUT_CAP) { g.err |= CIT_ERR_STEP_CAP; break; }
+    cit_random_step(g, rng, seer);
+    uint32_t* d = ring + (long)(n % max_move) * W;
+    for (int i = 0; i < W; i++) d[i] = gw[i];
+    n++;
+  }
+  if (g.err) return -1;
+  if (k > n) { g.err |= CIT_ERR_INDEX; return -1; }
+  const uint32_t* src = ring + (long)((n - k) % max_move) * W;
+  for (int i = 0; i < W; i++) gw[i] = src[i];
+  return n - k;
+}

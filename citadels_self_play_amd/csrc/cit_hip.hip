@@ -190,6 +190,23 @@ __global__ void k_advance(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t
   stage_out(lds, games, g0, nrows);
 }
 
+// create_a_random_game(max_move) per lane (train_from_scratch data generation).
+__global__ void k_random_position(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_move,
+                                  uint32_t* ring, int32_t* steps_out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  long g0 = (long)blockIdx.x * blockDim.x;
+  int nrows = (int)min((long)blockDim.x, (long)B - g0);
+  if (threadIdx.x < nrows) {
+    long l = g0 + threadIdx.x;
+    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
+    CitMT r = lane_mt(mt, idx, B, l);
+    steps_out[l] = cit_random_position(g, r, seer + l * CIT_SEER_MAX, ring + l * (long)max_move * ROW_W, max_move);
+    idx[l] = r.pos;
+  }
+  __syncthreads();
+  stage_out(lds, games, g0, nrows);
+}
+
 template <class K>
 int set_lds(K kernel, size_t bytes) {
   return (int)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -205,6 +222,7 @@ int ensure_attrs() {
   if (!e) e = set_lds(k_carry_out, m);
   if (!e) e = set_lds(k_rollout, m);
   if (!e) e = set_lds(k_advance, m);
+  if (!e) e = set_lds(k_random_position, m);
   if (!e) g_attrs_done = true;
   return e;
 }
@@ -304,6 +322,16 @@ int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
   const int G = 1;
   hipLaunchKernelGGL(k_advance, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx,
                      seer, B, lo, hi, steps);
+  CHECK_LAUNCH();
+}
+
+int cit_random_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_move,
+                        uint32_t* ring, int32_t* steps, hipStream_t stream) {
+  if (B <= 0 || max_move <= 0 || !games || !mt || !mt_idx || !seer || !ring || !steps) return -1;
+  if (int e = ensure_attrs()) return e;
+  const int G = 16;
+  hipLaunchKernelGGL(k_random_position, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+                     mt_idx, seer, B, max_move, ring, steps);
   CHECK_LAUNCH();
 }
 

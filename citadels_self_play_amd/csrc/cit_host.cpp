@@ -254,4 +254,30 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
   return waiting;
 }
 
+void cith_random_position(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_move,
+                          uint32_t* ring, int* steps) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    steps[l] = cit_random_position(g[l], r, seer + (long)l * CIT_SEER_MAX, ring, max_move);
+    SAVE(r);
+  }
+}
+
+void cith_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, const int* roots, int* counts) {
+  for (int l = 0; l < B; l++) {
+    CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+    cfr_count_targets(T, roots[l], counts[2 * l], counts[2 * l + 1]);
+  }
+}
+
+void cith_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, const int* roots, uint32_t* mt, uint32_t* idx,
+                      const int* offsets, int* meta, float* feat, double* value, double* dist, float* opt_feat) {
+  for (int l = 0; l < B; l++) {
+    CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+    CitMT r = lane_rng(mt, idx, B, l);
+    cfr_emit_targets(T, r, roots[l], l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
+    SAVE(r);
+  }
+}
+
 }  // extern "C"

@@ -130,6 +130,46 @@ class GameBatch:
                                            _stream()), "cit_cfr_decide")
         return chosen, stats
 
+    def random_position(self, max_move=100, seeds=None):
+        """random.seed(seed); create_a_random_game(max_move) (run_utils.py:55-73) on every
+        lane.  Returns steps into the game of each position (-1 on a lane error)."""
+        d = self.device
+        seeds = self.seeds if seeds is None else torch.as_tensor(np.asarray(seeds, np.int64)).to(d)
+        _lib.check(self.lib.cit_mt_seed(_ptr(self.mt), _ptr(self.mt_idx), self.B, _ptr(seeds), 0, _stream()),
+                   "cit_mt_seed")
+        ring = torch.empty(self.B * max_move * L.GAME_BYTES, dtype=torch.uint8, device=d)
+        steps = torch.zeros(self.B, dtype=torch.int32, device=d)
+        _lib.check(self.lib.cit_random_position(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.seer),
+                                                self.B, int(max_move), _ptr(ring), _ptr(steps), _stream()),
+                   "cit_random_position")
+        del ring
+        return steps
+
+    def cfr_targets(self, roots):
+        """get_all_targets over the trees of the last cfr_decide (roots = stats[:, 0]).
+        Returns a dict: meta [n,5] (lane, node, player override, n_children, first
+        option row), feat [n,418] f32, value [n,6] f64, dist [m] f64, opt_feat [m,131]
+        f32, counts [B,2]."""
+        d = self.device
+        roots = roots.to(device=d, dtype=torch.int32).contiguous()
+        counts = torch.zeros((self.B, 2), dtype=torch.int32, device=d)
+        _lib.check(self.lib.cit_cfr_target_count(_ptr(self.pool), self.B, self.node_cap, self.edge_cap, _ptr(roots),
+                                                 _ptr(counts), _stream()), "cit_cfr_target_count")
+        offs = torch.zeros_like(counts)
+        offs[1:] = torch.cumsum(counts, dim=0)[:-1]
+        tot = counts.sum(dim=0).cpu()
+        nt, nc = int(tot[0]), int(tot[1])
+        out = {"meta": torch.zeros((nt, 5), dtype=torch.int32, device=d),
+               "feat": torch.zeros((nt, 418), dtype=torch.float32, device=d),
+               "value": torch.zeros((nt, 6), dtype=torch.float64, device=d),
+               "dist": torch.zeros(nc, dtype=torch.float64, device=d),
+               "opt_feat": torch.zeros((nc, 131), dtype=torch.float32, device=d), "counts": counts}
+        _lib.check(self.lib.cit_cfr_targets(_ptr(self.pool), self.B, self.node_cap, self.edge_cap, _ptr(roots),
+                                            _ptr(self.mt), _ptr(self.mt_idx), _ptr(offs), _ptr(out["meta"]),
+                                            _ptr(out["feat"]), _ptr(out["value"]), _ptr(out["dist"]),
+                                            _ptr(out["opt_feat"]), _stream()), "cit_cfr_targets")
+        return out
+
     def _pool(self, node_cap, edge_cap):
         edge_cap = edge_cap or 8 * node_cap
         per = self.lib.cit_cfr_pool_bytes(node_cap, edge_cap)

@@ -156,6 +156,33 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
                       void* state, const float* probs, float* feat, CitOption* chosen, int32_t* waiting,
                       hipStream_t stream);
 
+/* ---- training-data generation (train_from_scratch.py:23-36 simulate_game) ---- */
+
+/* create_a_random_game(max_move) (run_utils.py:55-73) on every lane, whose
+ * CPython stream was seeded with cit_mt_seed (random.seed): k = randint(1,
+ * max_move), create_game(), a random playout to the winner, games[-k].  The
+ * stream continues from the end of the playout, as in the reference.  `ring`
+ * is scratch of B * max_move * cit_game_bytes() bytes (the last max_move
+ * snapshots of each lane).  steps[l] = steps into the game of the position,
+ * -1 on error (lane err bits set). */
+int cit_random_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_move,
+                        uint32_t* ring, int32_t* steps, hipStream_t stream);
+
+/* get_all_targets (deep_mccfr.py:258-274) / build_train_targets (:321-345)
+ * over the finished trees of cit_cfr_decide (same pool, roots = stats[:,0]).
+ * Threshold: build_train_targets' default 15 (get_all_targets does not pass
+ * its own).  Pass 1: counts[l] = {targets, option rows}.  Pass 2 (exclusive
+ * prefix sums of counts as offsets): per target k, meta[k] = {lane, node,
+ * player override (-1 none), n_children, first option row}, feat[k][418]
+ * (encode_game; a role-pick node draws randint(0,5) from the lane's CPython
+ * stream), value[k][6] = node_value (f64), dist[row] = regret target (f64),
+ * opt_feat[row][131] = encode_option of each child, rows in child order. */
+int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int32_t* counts,
+                         hipStream_t stream);
+int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, uint32_t* mt,
+                    uint32_t* mt_idx, const int32_t* offsets, int32_t* meta, float* feat, double* value, double* dist,
+                    float* opt_feat, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -420,3 +420,64 @@ def dfs(node, out):
     for _, c in node.children:
         dfs(c, out)
     return out
+
+
+# ------------------------------------------------------- training targets
+def random_position(seed, max_move=100):
+    """create_a_random_game(max_move) (run_utils.py:55-73) after random.seed(seed),
+    np.random.seed(seed): k = randint(1, max_move); a preset game played to the
+    end by random.choice, keeping a deep copy after every step; returns
+    (games[-k], np_rng).  The stream continues from the end of the playout."""
+    import random as _random
+    rng = _random.Random(seed)
+    k = rng.randint(1, max_move)
+    g = O.new_game(None, True, rng)
+    snaps = [clone(g)]
+    while True:
+        opts = g.get_options()
+        w = g.carry_out(opts[rng._randbelow(len(opts))])
+        snaps.append(clone(g))
+        if w is not None:
+            break
+    return snaps[-k], np.random.RandomState(seed)
+
+
+BUILD_THRESHOLD = 15    # build_train_targets' default; get_all_targets never passes its own (:268)
+
+
+def build_train_targets(node, rng):
+    """deep_mccfr.py:321-345 -> (encode_game f32[418], options f32[nch,131],
+    node_value f64[6], regret target f64[nch] or f64[10])."""
+    import mlp_oracle as M
+    if not node.children or node.nv.sum() < BUILD_THRESHOLD:
+        return []
+    opts = np.stack([M.encode_option(o) for o, _ in node.children])
+    if node.role_pick:
+        i = rng.randint(0, 5)
+        x = M.encode_game(node.game, i)
+        dist = np.array(node.R[i], dtype=np.float64)
+    else:
+        x = M.encode_game(node.game)
+        dist = np.array(node.R, dtype=np.float64)
+    if dist.sum() == 0:
+        dist = np.ones_like(dist)
+    return [(x, opts, node.nv.copy(), dist)]
+
+
+def get_all_targets(node, rng, out=None):
+    """get_all_targets (deep_mccfr.py:258-274): pre-order over the tree."""
+    out = [] if out is None else out
+    out += build_train_targets(node, rng)
+    for _, c in node.children:
+        get_all_targets(c, rng, out)
+    return out
+
+
+def simulate_game(seed, iters, max_move=100):
+    """simulate_game (train_from_scratch.py:23-36, pretrain: no model, training=True)
+    on a seeded position; returns (position, chosen, tree, targets) or raises like
+    the reference on a terminal position (action_choice on a childless root)."""
+    g, npr = random_position(seed, max_move)
+    pos = clone(g)
+    chosen, tr = run_mccfr(g, npr, iters, training=True)
+    return pos, chosen, tr, get_all_targets(tr.root, g.rng)

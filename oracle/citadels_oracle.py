@@ -194,9 +194,10 @@ class OPlayer:
 
 
 class OGame:
-    def __init__(self, seed, preset=True):
-        """Game.__init__ + set_preset / set_random_game + set_initial_variables (game.py:17-24,420-540)."""
-        self.rng = _random.Random(seed)
+    def __init__(self, seed, preset=True, rng=None):
+        """Game.__init__ + set_preset / set_random_game + set_initial_variables (game.py:17-24,420-540).
+        `rng` continues an existing stream instead of seeding a new one."""
+        self.rng = _random.Random(seed) if rng is None else rng
         if preset:
             deck = BASE_DECK + UNIQUE_DECK
         else:
@@ -1340,9 +1341,9 @@ def canon(g):
     return d
 
 
-def new_game(seed, preset=True):
+def new_game(seed, preset=True, rng=None):
     """run_utils.create_game (run_utils.py:20-27) with a per-game RNG seeded like random.seed(seed)."""
-    g = OGame(seed, preset)
+    g = OGame(seed, preset, rng)
     g.setup_round()
     return g
 

@@ -69,3 +69,60 @@ def encode_game(g, pid=None):
         rp = g.rp[r]
         v[378 + r * 5:378 + r * 5 + 5] = [bool(rp[0]), rp[1] is not None, bool(rp[2]), bool(rp[3]), rp[4] is not None]
     return v
+
+
+# option.py:33-49 (name_to_id order)
+OPTION_IDS = {n: i for i, n in enumerate([
+    "role_pick", "gold_or_card", "which_card_to_keep", "blackmail_response",
+    "reveal_blackmail_as_blackmailer", "reveal_warrant_as_magistrate", "build", "empty_option",
+    "finish_round", "ghost_town_color_choice", "smithy_choice", "laboratory_choice",
+    "magic_school_choice", "weapon_storage_choice", "lighthouse_choice", "museum_choice",
+    "graveyard", "take_gold_for_war", "assassination", "magistrate_warrant", "bewitching",
+    "steal", "blackmail", "spy", "magic_hand_change", "discard_and_draw", "look_at_hand",
+    "take_from_hand", "seer", "give_back_card", "take_crown_king", "give_crown",
+    "take_crown_pat", "bishop", "cardinal_exchange", "abbot_gold_or_card", "abbot_beg",
+    "merchant", "alchemist", "trader", "architect", "navigator_gold_card", "scholar",
+    "scholar_card_pick", "warlord_desctruction", "marshal_steal", "diplomat_exchange"])}
+NAMED = {"gold": 0, "card": 1, "pay": 2, "not_pay": 3, "reveal": 4, "not_reveal": 5, "4gold": 6, "4card": 7,
+         "trade": 8, "war": 9, "religion": 10, "lord": 11, "unique": 12}
+ROLE_IDS = dict({n: i // 3 for i, n in enumerate(O.ROLE_NAMES)}, Bewitched=-1)   # config.py:93 role_to_role_id
+
+
+def encode_option(o):
+    """option.encode_option (option.py:52-115) over a citadels_oracle.Opt: the
+    first matching attribute branch wins, in the reference's order."""
+    v = np.zeros(131, np.float32)
+    a = o.a
+    v[OPTION_IDS[o.name]] = 1
+    v[a["perpetrator"] + 47] = 1
+    ch = a.get("choice", None)
+    if "target" in a:
+        v[a["target"] + 53] = 1
+    elif "choice" in a and isinstance(ch, str) and ch in ROLE_IDS:
+        v[ROLE_IDS[ch] + 60] = 1
+    elif "choice" in a and isinstance(ch, str):
+        v[NAMED[ch] + 76] = 1
+    elif "choice" in a and isinstance(ch, O.Cd):
+        v[O.ctype(ch.code) + 89] = 1
+    elif "choice" in a and isinstance(ch, list):
+        for c in ch:
+            v[O.ctype(c.code) + 89] = 1
+    elif "built_card" in a:
+        v[O.ctype(a["built_card"].code) + 89] = 1
+    elif "real_target" in a:
+        v[a["real_target"] + 60] = 1
+    elif "fake_targets" in a:
+        v[a["fake_targets"][0] + 68] = 1
+        v[a["fake_targets"][1] + 68] = 1
+    elif "fake_target" in a:
+        v[a["fake_target"] + 68] = 1
+    elif "replica" in a:
+        v[129] = a["replica"]
+    elif "gold_or_card_combination" in a:
+        v[130] = list(a["gold_or_card_combination"]).count("card")
+    elif "chosen_card" in a:
+        v[O.ctype(a["chosen_card"].code) + 89] = 1
+    elif "cards_to_give" in a:
+        for c in a["cards_to_give"]:
+            v[O.ctype(c.code) + 89] = O.ctype(c.code)      # the type id itself, not 1 (option.py:113)
+    return v

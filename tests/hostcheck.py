@@ -165,3 +165,40 @@ def cfr_pred(cf, iters, max_depth, mlp):
         rounds += 1
     stats = np.stack([st[:, 8], st[:, 0], st[:, 1], st[:, 3], st[:, 2]], axis=1)
     return chosen, stats, rounds
+
+
+def random_position(hb, max_move=100):
+    """random.seed(seed); create_a_random_game(max_move) on every lane."""
+    lib().cith_mt_seed(_p(hb.mt), _p(hb.idx), C.c_int(hb.B), _p(hb.seeds), C.c_int(0))
+    ring = np.zeros(max_move * L.GAME_BYTES // 4, np.uint32)
+    steps = np.zeros(hb.B, np.int32)
+    lib().cith_random_position(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(hb.seer), C.c_int(hb.B), C.c_int(max_move),
+                               _p(ring), _p(steps))
+    return steps
+
+
+def cfr_targets(cf, roots):
+    """get_all_targets over every lane's finished tree -> dict of arrays (see cfr_emit_targets)."""
+    hb = cf.hb
+    roots = np.ascontiguousarray(roots, np.int32)
+    counts = np.zeros((hb.B, 2), np.int32)
+    lib().cith_cfr_target_count(_p(cf.pool), C.c_int(hb.B), C.c_int(cf.node_cap), C.c_int(cf.edge_cap), _p(roots),
+                                _p(counts))
+    offs = np.zeros_like(counts)
+    offs[1:] = np.cumsum(counts, axis=0)[:-1]
+    nt, nc = int(counts[:, 0].sum()), int(counts[:, 1].sum())
+    out = {"meta": np.zeros((nt, 5), np.int32), "feat": np.zeros((nt, 418), np.float32),
+           "value": np.zeros((nt, 6), np.float64), "dist": np.zeros(nc, np.float64),
+           "opt_feat": np.zeros((nc, 131), np.float32), "counts": counts}
+    lib().cith_cfr_targets(_p(cf.pool), C.c_int(hb.B), C.c_int(cf.node_cap), C.c_int(cf.edge_cap), _p(roots),
+                           _p(hb.mt), _p(hb.idx), _p(offs), _p(out["meta"]), _p(out["feat"]), _p(out["value"]),
+                           _p(out["dist"]), _p(out["opt_feat"]))
+    return out
+
+
+def split_targets(t):
+    """Per-lane lists of (feat, options [nch,131], node_value, regret target) tuples."""
+    per = [[] for _ in range(len(t["counts"]))]
+    for k, (lane, node, pid, nch, c0) in enumerate(t["meta"]):
+        per[lane].append((t["feat"][k], t["opt_feat"][c0:c0 + nch], t["value"][k], t["dist"][c0:c0 + nch]))
+    return per

@@ -1,0 +1,75 @@
+"""Training-data generation on a real MI355X through the C ABI
+(cit_random_position -> cit_cfr_decide(2000) -> cit_cfr_target_count /
+cit_cfr_targets) against the reference's own outputs
+(tests/golden/targets2000.json.gz), and batch-size invariance at scale."""
+import numpy as np
+import pytest
+import torch
+
+from citadels_self_play_amd import canon
+from citadels_self_play_amd import layout as L
+from conftest import load_golden
+from test_cfr_host_golden import hash_obj
+from test_targets_oracle_golden import check_targets
+
+pytestmark = pytest.mark.gpu
+
+
+def _split(t):
+    t = {k: v.cpu().numpy() for k, v in t.items()}
+    per = [[] for _ in range(len(t["counts"]))]
+    for k, (lane, node, pid, nch, c0) in enumerate(t["meta"]):
+        per[lane].append((t["feat"][k], t["opt_feat"][c0:c0 + nch], t["value"][k], t["dist"][c0:c0 + nch]))
+    return per
+
+
+def test_gpu_targets_golden():
+    from citadels_self_play_amd.engine import GameBatch
+    recs = load_golden("targets2000.json.gz")
+    b = GameBatch([r["seed"] for r in recs], preset=True)
+    b.random_position(100)
+    rows = b.rows()
+    for l, r in enumerate(recs):
+        assert canon.canon_game(L.game_from_bytes(rows[l])) == r["position"], r["seed"]
+    b.seed_numpy()
+    chosen, stats = b.cfr_decide(2000, node_cap=8192)
+    per = _split(b.cfr_targets(stats[:, 0]))
+    chosen, stats, rows = chosen.cpu().numpy(), stats.cpu().numpy(), b.rows()
+    mt = b.mt.cpu().numpy().view(np.uint32)
+    idx = b.mt_idx.cpu().numpy()
+    npmt = b.np_mt.cpu().numpy().view(np.uint32)
+    npidx = b.np_idx.cpu().numpy()
+    for l, r in enumerate(recs):
+        root, n_nodes, n_edges, carry, err = stats[l]
+        assert err == 0, r["seed"]
+        assert n_nodes == r["nodes"] and carry == r["carry_outs"], r["seed"]
+        g = L.game_from_bytes(rows[l])
+        assert canon.canon_option(L.opt_from_bytes(chosen[l]), g) == r["chosen"], r["seed"]
+        assert hash_obj(mt[:, l].tolist() + [int(idx[l])]) == r["rng_after"][0], r["seed"]
+        assert hash_obj(npmt[:, l].tolist()) == r["rng_after"][1] and int(npidx[l]) == r["rng_after"][2]
+        check_targets(per[l], r["targets"], r["seed"])
+
+
+def test_gpu_targets_batch_invariance():
+    """512 trees of cfr_train(500): every lane's targets are the same whether it
+    runs in the full batch or in a strided sub-batch."""
+    from citadels_self_play_amd.engine import GameBatch
+    seeds = np.arange(7_000_000, 7_000_512)
+    out = []
+    for sel in (slice(None), slice(None, None, 37)):
+        b = GameBatch(seeds[sel], preset=True)
+        steps = b.random_position(100).cpu().numpy()
+        assert (steps >= 0).all()
+        b.seed_numpy()
+        chosen, stats = b.cfr_decide(500, node_cap=4096)
+        t = b.cfr_targets(stats[:, 0])
+        torch.cuda.synchronize()
+        out.append((stats.cpu().numpy(), _split(t)))
+    (s_all, t_all), (s_sub, t_sub) = out
+    assert np.array_equal(s_all[::37, 1:], s_sub[:, 1:])
+    assert sum(len(x) for x in t_all) > 100
+    for a, bb in zip(t_all[::37], t_sub):
+        assert len(a) == len(bb)
+        for x, y in zip(a, bb):
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v)

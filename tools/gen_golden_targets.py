@@ -1,0 +1,88 @@
+"""Golden fixtures for the training-data path of train_from_scratch
+("config 5") from the reference itself (build container only; writes
+tests/golden/targets2000.json.gz).
+
+Harness, per seed s (simulate_game, train_from_scratch.py:23-36, pretrain):
+    random.seed(s); np.random.seed(s)
+    game = create_a_random_game(100)                        # run_utils.py:55-73
+    _, root = run_mccfr(game, None, max_iterations=M, training=True)   # run_utils.py:75-87
+    targets = root.get_all_targets(usefulness_treshold=200) # deep_mccfr.py:258-274,321-345
+
+Recorded per seed: the position, node / carry_out counts, the chosen option,
+RNG end states, and every target tuple: encode_game row (small ints), the
+options' encode_option rows (sha256 of the float32 bytes + shape),
+node_value and the regret target (float64 lists).  `seaborn` is stubbed.
+"""
+import gzip
+import hashlib
+import json
+import os
+import random
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "..", "tests", "golden")
+sys.path.insert(0, HERE)
+sys.path.insert(0, REF)
+sys.modules.setdefault("seaborn", types.ModuleType("seaborn"))
+
+import refcanon as rc  # noqa: E402
+from gen_golden_cfr import count_nodes  # noqa: E402
+
+
+def case(seed, iters):
+    import game.option as gopt
+    from run_utils import create_a_random_game, run_mccfr
+    random.seed(seed)
+    np.random.seed(seed)
+    g = create_a_random_game(100)
+    rec = {"seed": seed, "iters": iters, "position": rc.canon_game(g)}
+    counter = [0]
+    orig = gopt.option.carry_out
+
+    def counting(self, game):
+        counter[0] += 1
+        return orig(self, game)
+
+    gopt.option.carry_out = counting
+    try:
+        chosen, root = run_mccfr(g, model=None, max_iterations=iters, training=True)
+    except Exception as e:           # a terminal position: action_choice on a childless root
+        rec["error"] = type(e).__name__
+        return rec
+    finally:
+        gopt.option.carry_out = orig
+    rec["error"] = None
+    rec["carry_outs"] = counter[0]
+    rec["nodes"] = count_nodes(root)
+    rec["chosen"] = rc.canon_option(chosen)
+    targets = root.get_all_targets(usefulness_treshold=200)
+    rec["rng_after"] = [rc.hash_obj(list(random.getstate()[1])), rc.hash_obj(np.random.get_state()[1].tolist()),
+                        int(np.random.get_state()[2])]
+    tl = []
+    for x, opts, nv, dist in targets:
+        o = opts.detach().numpy().astype(np.float32)
+        tl.append({"encode": [int(v) for v in x.tolist()],
+                   "opts_shape": list(o.shape), "opts_sha": hashlib.sha256(o.tobytes()).hexdigest()[:32],
+                   "nv": np.asarray(nv.numpy(), np.float64).tolist(),
+                   "dist": np.asarray(dist.numpy(), np.float64).tolist()})
+    rec["targets"] = tl
+    return rec
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    recs = []
+    for s in range(16):
+        recs.append(case(s, 2000))
+        print(s, recs[-1].get("error"), recs[-1].get("nodes"), len(recs[-1].get("targets", [])), flush=True)
+    with gzip.open(os.path.join(OUT, "targets2000.json.gz"), "wt") as f:
+        json.dump(recs, f, separators=(",", ":"))
+
+
+if __name__ == "__main__":
+    main()

@@ -36,9 +36,12 @@ _SIGS = {
     "cit_advance_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp], i32),
     "cit_cfr_decide": ([vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, vp], i32),
     "cit_cfr_state_bytes": ([], i32),
+    "cit_randbelow": ([vp, vp, i32, i32, vp, vp], i32),
     "cit_random_position": ([vp, vp, vp, vp, i32, i32, vp, vp, vp], i32),
-    "cit_cfr_target_count": ([vp, i32, i32, i32, vp, vp, vp], i32),
-    "cit_cfr_targets": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    "cit_cfr_target_count": ([vp, i32, i32, i32, vp, i32, vp, vp], i32),
+    "cit_cfr_targets": ([vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    "cit_close_rows": ([], i32),
+    "cit_close_position": ([vp, vp, vp, vp, i32, vp, vp, vp], i32),
     "cit_cfr_pred_step": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp], i32),
 }
 

@@ -1,0 +1,656 @@
+"""The reference's object API over device-resident games.
+
+    from citadels_self_play_amd import api
+    api.seed(0)                                   # random.seed(0); np.random.seed(0)
+    game = api.create_game()                      # run_utils.create_game (run_utils.py:20-27)
+    options = game.get_options_from_state()       # Game.get_options_from_state (game.py:415-418)
+    winner = options[0].carry_out(game)           # option.carry_out (option.py:118-122)
+    x = game.encode_game()                        # Game.encode_game (game.py:34-128)
+    chosen, root = api.run_mccfr(game)            # run_utils.run_mccfr (run_utils.py:74-87)
+    targets = root.get_all_targets(200)           # CFRNode.get_all_targets (deep_mccfr.py:258-274)
+
+Every `Game` is one packed row in HBM; every call is one launch of the same
+HIP kernels the batched drivers use (engine.GameBatch with B = 1), so a
+facade game and a batch lane with the same seed walk identical trajectories.
+This is the compatibility path (one game per launch); throughput comes from
+engine.GameBatch / selfplay.py.
+
+Randomness: the reference draws from the process-wide `random` and
+`np.random` modules.  Here a `Stream` holds one CPython MT19937 and one numpy
+MT19937 on the device; games created from a stream (and their deep copies)
+share it, as the reference's games share the module state.  `seed(s)` resets
+the default stream like `random.seed(s); np.random.seed(s)`.
+
+Errors surface as the reference's exception types (IndexError on an empty
+option list, ValueError from np.random.choice, KeyError, ...), raised from
+the lane's error bits after each call.
+
+Differences, by design:
+* `CFRNode(game, ...)` defers skip_false_choice (deep_mccfr.py:37-49) to the
+  search call; `cfr_train`/`cfr_pred` mutate `game` exactly as the reference's
+  constructor would, before anything can observe it.
+* The search and the live decision run in one launch (what run_mccfr does);
+  `action_choice(live=True)` returns that decision.  `action_choice(live=False)`
+  (the in-search sampler) is internal to the device search.
+"""
+import copy as _copy
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import layout as L
+from .canon import deck_list, kh_entries
+from .rules import OPTION_NAMES, ROLE_NAMES, SUITS, card_cost, card_suit, card_type
+
+
+def _ptr(t):
+    return t.data_ptr()
+
+
+def _cs():
+    return torch.cuda.current_stream().cuda_stream
+
+
+_ERR_TYPES = [(0x2, IndexError, "Cannot choose from an empty sequence"), (0x10, IndexError, "list index out of range"),
+              (0x4, KeyError, "role_properties[-1]"), (0x8, ValueError, "probabilities / list.remove"),
+              (0x20, AttributeError, "NoneType"), (0x80, TypeError, "get_options returned None"),
+              (0x1, OverflowError, "a fixed-capacity container overflowed"),
+              (0x40, NotImplementedError, "unsupported branch"), (0x100, RuntimeError, "step cap")]
+
+
+def raise_for(err, what=""):
+    """The reference's exception for a lane error word (CIT_ERR_* bits)."""
+    for bit, exc, msg in _ERR_TYPES:
+        if err & bit:
+            raise exc("%s%s (engine error 0x%x)" % (what + ": " if what else "", msg, err))
+
+
+# ------------------------------------------------------------------ streams
+class Stream:
+    """One process's `random` (CPython MT19937) and `np.random` (numpy MT19937) on the device."""
+
+    def __init__(self, seed=0, device=None):
+        if not torch.cuda.is_available():
+            raise _lib.NativeError("the api needs a GPU (the engine has no CPU fallback)")
+        self.lib = _lib.load()
+        self.device = torch.device(device or "cuda")
+        d = self.device
+        self.mt = torch.zeros((L.MT_N, 1), dtype=torch.int32, device=d)
+        self.idx = torch.zeros(1, dtype=torch.int32, device=d)
+        self.np_mt = torch.zeros((L.MT_N, 1), dtype=torch.int32, device=d)
+        self.np_idx = torch.zeros(1, dtype=torch.int32, device=d)
+        self.seed(seed)
+
+    def seed(self, s, numpy_seed=None):
+        """random.seed(s); np.random.seed(numpy_seed if given else s)."""
+        d = self.device
+        a = torch.tensor([int(s)], dtype=torch.int64, device=d)
+        b = torch.tensor([int(s if numpy_seed is None else numpy_seed)], dtype=torch.int64, device=d)
+        _lib.check(self.lib.cit_mt_seed(_ptr(self.mt), _ptr(self.idx), 1, _ptr(a), 0, _cs()), "cit_mt_seed")
+        _lib.check(self.lib.cit_mt_seed(_ptr(self.np_mt), _ptr(self.np_idx), 1, _ptr(b), 1, _cs()), "cit_mt_seed")
+
+    def randint(self, a, b):
+        """random.randint(a, b) from this stream (randrange(a, b+1) via _randbelow)."""
+        out = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_randbelow(_ptr(self.mt), _ptr(self.idx), 1, int(b - a + 1), _ptr(out), _cs()),
+                   "cit_randbelow")
+        return a + int(out.item())
+
+
+_default = {}
+
+
+def default_stream(device=None):
+    d = torch.device(device or "cuda")
+    if d not in _default:
+        _default[d] = Stream(0, d)
+    return _default[d]
+
+
+def seed(s, device=None):
+    """random.seed(s); np.random.seed(s) for the default stream."""
+    default_stream(device).seed(s)
+
+
+# -------------------------------------------------------------- value views
+class Card:
+    """game/deck.py:7-24: equality and ordering by type_ID only."""
+    __slots__ = ("suit", "type_ID", "cost", "code")
+
+    def __init__(self, code):
+        self.code = int(code)
+        self.type_ID = card_type(self.code)
+        self.suit = SUITS[card_suit(self.code)]
+        self.cost = card_cost(self.code)
+
+    def __eq__(self, o):
+        return isinstance(o, Card) and self.type_ID == o.type_ID
+
+    def __lt__(self, o):
+        return isinstance(o, Card) and self.type_ID < o.type_ID
+
+    def __hash__(self):
+        return hash(self.type_ID)
+
+    def __repr__(self):
+        return "Card(%d, %s, %d)" % (self.type_ID, self.suit, self.cost)
+
+
+class Deck:
+    def __init__(self, codes):
+        self.cards = [Card(c) for c in codes]
+
+    def __len__(self):
+        return len(self.cards)
+
+    def __eq__(self, o):
+        return isinstance(o, Deck) and self.cards == o.cards
+
+
+class GameState:
+    """helper_classes.py:16-34 (a read-only view); equality on state and player only."""
+
+    def __init__(self, state, pid, adm, intr, nxt=None):
+        self.state, self.player_id, self.interruption, self.next_gamestate = state, pid, bool(intr), nxt
+        self.already_done_moves = [t for t, n in zip(_ADM, adm) for _ in range(n)]
+
+    def __eq__(self, o):
+        return isinstance(o, GameState) and self.state == o.state and self.player_id == o.player_id
+
+
+_ADM = ["begged", "character_ability", "lab", "magic_school", "museum", "non_trade_building", "smithy", "take_gold",
+        "trade_building"]
+
+
+class Agent:
+    """game/agent.py:10-29 (a read-only view of one player of a game row)."""
+
+    def __init__(self, g, i, khs):
+        p = g.pl[i]
+        self.id = i
+        self.hand = Deck(p.hand[:p.n_hand])
+        self.buildings = Deck(p.build[:p.n_build])
+        self.just_drawn_cards = Deck(p.jd[:p.n_jd])
+        self.museum_cards = Deck(p.museum[:p.n_museum])
+        self.gold = int(p.gold)
+        self.role = None if p.role == L.ROLE_NONE else ("Bewitched" if p.role == L.ROLE_BEWITCHED
+                                                         else ROLE_NAMES[p.role])
+        self.replicas = int(p.replicas)
+        self.crown = bool(p.flags & 1)
+        self.can_use_lighthouse = bool(p.flags & 2)
+        self.first_to_7 = bool(p.flags & 4)
+        self.witch = bool(p.flags & 8)
+        self.known_roles = [(int(p.kr[j]) & 0x1FF, bool((int(p.kr[j]) >> 15) & 1)) for j in range(6)]
+        self.known_hands = [(t, c, w, u, [Card(x) for x in cards]) for (o, t, c, w, u, cards) in khs if o == i]
+
+    def __eq__(self, o):
+        return isinstance(o, Agent) and self.id == o.id
+
+    def __repr__(self):
+        return "Agent(%d)" % self.id
+
+
+# -------------------------------------------------------------------- games
+class Game:
+    """One game row in HBM (game/game.py Game).  `Game(preset)` is
+    run_utils.create_game(): Game(preset) followed by setup_round()."""
+
+    def __init__(self, preset=False, stream=None, device=None, _row=None):
+        self.stream = stream or default_stream(device)
+        self.lib = self.stream.lib
+        self.device = self.stream.device
+        d = self.device
+        self.seer = torch.zeros((1, L.SEER_MAX), dtype=torch.int64, device=d)
+        if _row is not None:
+            self.row = _row
+        else:
+            self.row = torch.zeros((1, L.GAME_BYTES), dtype=torch.uint8, device=d)
+            _lib.check(self.lib.cit_init(_ptr(self.row), _ptr(self.stream.mt), _ptr(self.stream.idx), 1, None,
+                                         int(bool(preset)), _cs()), "cit_init")
+        self._view = None
+
+    # -- plumbing
+    def _dirty(self):
+        self._view = None
+
+    def packed(self):
+        """The CitGame view of the row (host copy, cached until the next mutation)."""
+        if self._view is None:
+            self._view = L.game_from_bytes(self.row[0].cpu().numpy())
+        return self._view
+
+    def _check(self, what):
+        e = int(self.packed().err)
+        if e:
+            raise_for(e, what)
+
+    def __deepcopy__(self, memo):
+        g = Game(stream=self.stream, _row=self.row.clone())
+        g.seer.copy_(self.seer)
+        return g
+
+    # -- state
+    @property
+    def players(self):
+        g = self.packed()
+        khs = kh_entries(g)
+        return [Agent(g, i, khs) for i in range(6)]
+
+    @property
+    def gamestate(self):
+        g = self.packed()
+        nxt = None
+        if g.nx_valid:
+            nxt = GameState(int(g.nx_state), int(g.nx_pid), list(g.nx_adm), g.nx_intr)
+        return GameState(int(g.gs_state), int(g.gs_pid), list(g.gs_adm), g.gs_intr, nxt)
+
+    @property
+    def terminal(self):
+        return bool(self.packed().terminal)
+
+    @property
+    def ending(self):
+        return bool(self.packed().ending)
+
+    @property
+    def rewards(self):
+        g = self.packed()
+        r = np.zeros(6)
+        if g.winner >= 0:
+            r[g.winner] = 1
+        return r
+
+    @property
+    def roles(self):
+        return {i: ROLE_NAMES[r] for i, r in enumerate(self.packed().roles)}
+
+    @property
+    def turn_orders_for_roles(self):
+        return list(self.packed().turn)
+
+    @property
+    def deck(self):
+        return Deck(deck_list(self.packed()))
+
+    # -- step API
+    def get_options_from_state(self, max_opts=4096):
+        opts = torch.zeros((1, max_opts, 16), dtype=torch.uint8, device=self.device)
+        n = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_get_options(_ptr(self.row), _ptr(self.stream.mt), _ptr(self.stream.idx),
+                                            _ptr(self.seer), 1, _ptr(opts), max_opts, _ptr(n), _cs()),
+                   "cit_get_options")
+        self._dirty()
+        self._check("get_options_from_state")
+        k = int(n.item())
+        if k > max_opts:
+            return self.get_options_from_state(k)
+        g = self.packed()
+        host = opts[0, :k].cpu().numpy()
+        return [Option(host[i], g) for i in range(k)]
+
+    def encode_game(self):
+        feat = torch.zeros((1, 418), dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.cit_encode_games(_ptr(self.row), 1, -1, _ptr(feat), _cs()), "cit_encode_games")
+        return feat[0].cpu()
+
+    def __repr__(self):
+        gs = self.gamestate
+        return "Game(state=%d, player=%d, terminal=%s)" % (gs.state, gs.player_id, self.terminal)
+
+
+def _typed_attrs(o, g):
+    """option.attributes (the generators of game/agent_functions.py) decoded from a descriptor."""
+    n = OPTION_NAMES[o.name]
+    p = o.perp
+    a = {"perpetrator": p}
+
+    def s8(v):
+        return v - 256 if v >= 128 else v
+
+    def cards_of(mask, hand):
+        return [Card(hand[i]) for i in range(64) if (mask >> i) & 1]
+
+    if n == "role_pick":
+        a["choice"] = ROLE_NAMES[g.roles[o.a]]
+    elif n == "gold_or_card":
+        a["choice"] = ["gold", "card"][o.a]
+    elif n == "which_card_to_keep":
+        cs = [Card(o.a)] if o.b == L.NO_CARD else [Card(o.a), Card(o.b)]
+        a["choice"] = tuple(cs) if o.flags & 1 else cs
+    elif n == "blackmail_response":
+        a["choice"] = ["pay", "not_pay"][o.a]
+    elif n in ("reveal_blackmail_as_blackmailer", "reveal_warrant_as_magistrate"):
+        a["choice"] = ["reveal", "not_reveal"][o.a]
+        a["target"] = s8(o.target)
+    elif n == "build":
+        a["built_card"] = Card(o.a)
+        a["replica"] = s8(o.c)
+    elif n == "empty_option":
+        a["next_gamestate"] = (GameState(5, p, [0] * 9, False) if o.a == 0 else
+                               GameState(int(g.nx_state), int(g.nx_pid), list(g.nx_adm), g.nx_intr))
+    elif n == "finish_round":
+        a["next_witch"] = bool(o.flags & 1)
+        a["crown"] = bool(o.flags & 2)
+    elif n in ("laboratory_choice", "lighthouse_choice", "museum_choice"):
+        a["choice"] = Card(o.a)
+    elif n == "magic_school_choice":
+        a["choice"] = SUITS[o.a]
+    elif n in ("weapon_storage_choice", "warlord_desctruction", "marshal_steal"):
+        a["target"] = s8(o.target)
+        a["choice"] = Card(o.a)
+    elif n in ("assassination", "bewitching", "steal"):
+        a["choice"] = o.a
+    elif n == "magistrate_warrant":
+        a["real_target"] = o.a
+        a["fake_targets"] = [o.b, o.c]
+    elif n == "blackmail":
+        a["real_target"] = o.a
+        a["fake_target"] = o.b
+    elif n == "spy":
+        a["target"] = s8(o.target)
+        a["suit"] = SUITS[o.a]
+    elif n in ("magic_hand_change", "look_at_hand"):
+        a["target"] = s8(o.target)
+    elif n == "discard_and_draw":
+        a["cards"] = cards_of(o.x, g.pl[p].hand)
+    elif n == "take_from_hand":
+        a["target"] = s8(o.target)
+        if o.flags & 1:
+            a["built_card"] = Card(o.a)
+            a["build"] = True
+            a["replica"] = s8(o.c)
+        else:
+            a["card"] = Card(o.a)
+            a["build"] = False
+    elif n == "give_back_card":
+        a["card_handouts"] = {int(g.seer_from[i]): Card((o.x >> (8 * i)) & 0xFF) for i in range(o.b)}
+    elif n == "give_crown":
+        a["target"] = s8(o.target)
+        a["gold_or_card"] = ["card", "gold", "nothing"][o.a]
+    elif n == "cardinal_exchange":
+        a["target"] = s8(o.target)
+        a["built_card"] = Card(o.a)
+        a["cards_to_give"] = cards_of(o.x, g.pl[p].hand)
+        a["replica"] = s8(o.c)
+        a["factory"] = bool(o.flags & 1)
+    elif n == "abbot_gold_or_card":
+        a["gold_or_card_combination"] = ["gold"] * (o.a - o.b) + ["card"] * o.b
+    elif n == "navigator_gold_card":
+        a["choice"] = ["4gold", "4card"][o.a]
+    elif n == "scholar_card_pick":
+        a["choice"] = Card(o.a)
+        a["chosen_card"] = Card(o.a)
+        a["unchosen_cards"] = Deck(g.seven[:g.n_seven])
+    elif n == "diplomat_exchange":
+        a["target"] = s8(o.target)
+        a["choice"] = Card(o.a)
+        a["give"] = Card(o.b)
+        a["money_owed"] = o.c
+    return n, a
+
+
+class Option:
+    """game/option.py option: `name`, `attributes`, carry_out, encode_option.
+    Holds the 16-byte device descriptor it was enumerated as."""
+
+    def __init__(self, desc, g=None):
+        self.desc = np.ascontiguousarray(desc, np.uint8).copy()
+        o = L.opt_from_bytes(self.desc)
+        self.name, self.attributes = _typed_attrs(o, g) if g is not None else (OPTION_NAMES[o.name], {})
+
+    def __eq__(self, o):
+        return isinstance(o, Option) and self.name == o.name and self.attributes == o.attributes
+
+    def __str__(self):
+        return "%s, %s" % (self.name, self.attributes)
+
+    __repr__ = __str__
+
+    def carry_out(self, game):
+        """Mutates `game`; returns the winning Agent or None (option.py:118-122)."""
+        d = torch.from_numpy(self.desc).to(game.device).reshape(1, 16)
+        w = torch.zeros(1, dtype=torch.int32, device=game.device)
+        _lib.check(game.lib.cit_carry_out(_ptr(game.row), _ptr(game.stream.mt), _ptr(game.stream.idx), 1, _ptr(d),
+                                          _ptr(w), _cs()), "cit_carry_out")
+        game._dirty()
+        game._check("carry_out(%s)" % self.name)
+        wi = int(w.item())
+        return game.players[wi] if wi >= 0 else None
+
+    def encode_option(self, game=None):
+        """[1, 131] float32 (option.py:52-115)."""
+        lib = _lib.load()
+        dev = game.device if game is not None else torch.device("cuda")
+        row = game.row if game is not None else torch.zeros((1, L.GAME_BYTES), dtype=torch.uint8, device=dev)
+        d = torch.from_numpy(self.desc).to(dev).reshape(1, 16)
+        lane = torch.zeros(1, dtype=torch.int32, device=dev)
+        out = torch.zeros((1, 131), dtype=torch.float32, device=dev)
+        _lib.check(lib.cit_encode_options(_ptr(row), _ptr(d), _ptr(lane), 1, _ptr(out), _cs()), "cit_encode_options")
+        return out.cpu()
+
+
+# ------------------------------------------------------------------- search
+class CFRNode:
+    """algorithms/deep_mccfr.py CFRNode.  The root owns a device node pool; child
+    nodes are views into it (node_value, cumulative_regrets, strategy, children)."""
+
+    def __init__(self, game, original_player_id, parent=None, player_count=6, model=None, training=False,
+                 device=None, model_reward_weights=5, depth=0, node_cap=None):
+        if parent is not None:
+            raise ValueError("child nodes are created by the search")
+        self.game = game
+        self.original_player_id = original_player_id
+        self.model = model
+        self.training = training
+        self.node_cap = node_cap
+        self._tree = None
+        self._chosen = None
+
+    # -- search
+    def _batch(self):
+        from .engine import GameBatch
+        st = self.game.stream
+        return GameBatch.from_tensors(self.game.row, st.mt, st.idx, self.game.seer, st.np_mt, st.np_idx)
+
+    def cfr_train(self, max_iterations=100000):
+        """cfr_train (deep_mccfr.py:187-205) + the live decision of run_mccfr."""
+        b = self._batch()
+        chosen, stats = b.cfr_decide(max_iterations, node_cap=self.node_cap or max(1024, 4 * max_iterations))
+        self._finish(b, chosen, stats)
+
+    def cfr_pred(self, max_iterations=2000, max_depth=20):
+        """cfr_pred (deep_mccfr.py:207-229) with value-net leaves + the live decision."""
+        from .models import ValueNet
+        net = self.model if isinstance(self.model, ValueNet) else ValueNet(self.model, self.game.device)
+        b = self._batch()
+        chosen, stats, _ = b.cfr_pred(max_iterations, net, max_depth=max_depth,
+                                      node_cap=self.node_cap or max(2048, 4 * max_iterations))
+        self._finish(b, chosen, stats)
+
+    def _finish(self, b, chosen, stats):
+        self.game._dirty()
+        st = stats.cpu().numpy()[0]
+        self._stats = st
+        self._b = b
+        root, err = int(st[0]), int(st[4])
+        self._tree = None
+        self._root = root
+        self._chosen = chosen[0].cpu().numpy()
+        self._err = err
+
+    def action_choice(self, live=False):
+        if not live:
+            raise NotImplementedError("the in-search sampler runs inside the device search")
+        if self._chosen is None:
+            raise RuntimeError("call cfr_train / cfr_pred first")
+        if self._err:
+            raise_for(self._err, "action_choice")
+        return None, Option(self._chosen, self.game.packed())
+
+    # -- tree views
+    def _load(self):
+        if self._tree is None:
+            self._tree = self._b.tree(0)
+        return self._tree
+
+    def _node(self, n):
+        return _NodeView(self, n)
+
+    @property
+    def root(self):
+        return self._node(self._root)
+
+    def __getattr__(self, k):
+        if k in ("node_value", "cumulative_regrets", "strategy", "cumulative_strategy", "winning_probabilities",
+                 "children", "depth", "role_pick_node", "get_all_targets", "build_train_targets"):
+            return getattr(self.root, k)
+        raise AttributeError(k)
+
+    @property
+    def carry_outs(self):
+        return int(self._stats[3])
+
+    @property
+    def node_count(self):
+        return int(self._stats[1])
+
+
+class _NodeView:
+    def __init__(self, owner, n):
+        self.owner, self.n = owner, n
+        nodes, edges, rows = owner._load()
+        self._N = nodes[n]
+        self._E = edges[self._N["first_edge"]:self._N["first_edge"] + self._N["n_children"]] \
+            if self._N["n_children"] > 0 else edges[:0]
+        self._row = rows[n]
+
+    @property
+    def role_pick_node(self):
+        return bool(self._N["flags"] & 1)
+
+    @property
+    def depth(self):
+        return int(self._N["depth"])
+
+    @property
+    def node_value(self):
+        return np.array(self._N["nv"])
+
+    @property
+    def winning_probabilities(self):
+        return np.array(self._N["wp"])
+
+    def _arr(self, f):
+        if self.role_pick_node:
+            return np.array(self._E[f]).T.copy()           # [6, 10]
+        return np.array(self._E[f][:, 0])
+
+    @property
+    def cumulative_regrets(self):
+        return self._arr("R")
+
+    @property
+    def strategy(self):
+        return self._arr("S")
+
+    @property
+    def cumulative_strategy(self):
+        return self._arr("CS")
+
+    @property
+    def game(self):
+        return L.game_from_bytes(self._row)
+
+    @property
+    def children(self):
+        g = self.game
+        return [(Option(e["opt"], g), _NodeView(self.owner, int(e["child"]))) for e in self._E]
+
+    def get_all_targets(self, usefulness_treshold=15):
+        """(deep_mccfr.py:258-274) over this node's subtree: a list of
+        (encode_game f32[418], options f32[1,nch,131], node_value f64[6], target f64)."""
+        return self._targets(0)
+
+    def build_train_targets(self, usefulness_treshold=15):
+        raise NotImplementedError("use get_all_targets (targets are built on the device)")
+
+    def _targets(self, mode):
+        b = self.owner._b
+        t = b.cfr_targets(torch.tensor([self.n], dtype=torch.int32), mode=mode)
+        t = {k: v.cpu() for k, v in t.items()}
+        out = []
+        for k, (lane, node, pid, nch, c0) in enumerate(t["meta"].tolist()):
+            out.append((t["feat"][k], t["opt_feat"][c0:c0 + nch].unsqueeze(0), t["value"][k],
+                        t["dist"][c0:c0 + nch]))
+        self.owner.game._dirty()
+        return out
+
+
+# --------------------------------------------------------------- run_utils
+def create_game(stream=None, device=None):
+    """run_utils.create_game (run_utils.py:20-27): Game(preset=True) + setup_round()."""
+    return Game(preset=True, stream=stream, device=device)
+
+
+def create_a_random_game(max_move_num, stream=None, device=None):
+    """run_utils.create_a_random_game (run_utils.py:55-73)."""
+    st = stream or default_stream(device)
+    g = Game(stream=st, _row=torch.zeros((1, L.GAME_BYTES), dtype=torch.uint8, device=st.device))
+    ring = torch.empty(max_move_num * L.GAME_BYTES, dtype=torch.uint8, device=st.device)
+    steps = torch.zeros(1, dtype=torch.int32, device=st.device)
+    _lib.check(st.lib.cit_random_position(_ptr(g.row), _ptr(st.mt), _ptr(st.idx), _ptr(g.seer), 1, int(max_move_num),
+                                          _ptr(ring), _ptr(steps), _cs()), "cit_random_position")
+    g._check("create_a_random_game")
+    return g
+
+
+def create_a_close_to_finished_game(game):
+    """run_utils.create_a_close_to_finished_game (run_utils.py:29-53); plays `game`
+    to the end like the reference and returns the picked snapshot."""
+    st = game.stream
+    out = Game(stream=st, _row=game.row.clone())
+    store = torch.empty(st.lib.cit_close_rows() * L.GAME_BYTES, dtype=torch.uint8, device=st.device)
+    index = torch.zeros(1, dtype=torch.int32, device=st.device)
+    _lib.check(st.lib.cit_close_position(_ptr(out.row), _ptr(st.mt), _ptr(st.idx), _ptr(out.seer), 1, _ptr(store),
+                                         _ptr(index), _cs()), "cit_close_position")
+    out._check("create_a_close_to_finished_game")
+    return out
+
+
+def run_mccfr(game, model=None, max_iterations=2000, training=False):
+    """run_utils.run_mccfr (run_utils.py:74-87)."""
+    root = CFRNode(game, original_player_id=game.gamestate.player_id, model=model, training=training)
+    if model is not None and not training:
+        root.cfr_pred(max_iterations=max_iterations, max_depth=10)
+    else:
+        root.cfr_train(max_iterations=max_iterations)
+    _, chosen = root.action_choice(live=True)
+    return chosen, root
+
+
+def encode_options_from_node(node):
+    """run_utils.encode_options_from_node (run_utils.py:89-97): [1, nch, 131]."""
+    kids = node.children
+    if not kids:
+        return []
+    return torch.cat([o.encode_option() for o, _ in kids], dim=0).unsqueeze(0)
+
+
+def create_target_strategy(node):
+    """run_utils.create_target_strategy (run_utils.py:98-109) at a search root."""
+    view = node.root if isinstance(node, CFRNode) else node
+    t = view._targets(1)
+    if not t:
+        raise ValueError("node has no children")
+    return t[0][3]
+
+
+def setup_model_for_eval(model_path, device=None):
+    """run_utils.setup_model_for_eval for a state_dict this framework (or the
+    user) saved: weights_only loading, eval mode, device-resident MFMA form."""
+    from .models import ValueNet, ValueOnlyNN
+    m = ValueOnlyNN(418, hidden_size=512)
+    m.load_state_dict(torch.load(model_path, map_location="cpu", weights_only=True))
+    m.eval()
+    return ValueNet(m, device or "cuda")

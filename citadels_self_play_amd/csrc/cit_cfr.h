@@ -692,13 +692,14 @@ CIT_HD bool cfr_is_target(const CfrTree& T, int n) {
   return s >= CFR_TARGET_THRESHOLD;
 }
 
-// Pre-order successor through parent links (-1 after the last node).
-CIT_HD int cfr_preorder_next(const CfrTree& T, int n) {
+// Pre-order successor within the subtree of `top` through parent links (-1
+// after its last node).
+CIT_HD int cfr_preorder_next(const CfrTree& T, int n, int top) {
   const CfrNode& N = T.nodes[n];
   if (N.n_children > 0) return T.edges[N.first_edge].child;
   for (;;) {
     int p = T.nodes[n].parent;
-    if (p < 0) return -1;
+    if (n == top || p < 0) return -1;
     const CfrNode& P = T.nodes[p];
     int j = 0;
     while (j < P.n_children && T.edges[P.first_edge + j].child != n) j++;
@@ -720,12 +721,24 @@ CIT_HD CfrTree cfr_tree_view(uint8_t* pool, long l, int node_cap, int edge_cap) 
   return T;
 }
 
+// Target modes: CFR_TGT_TREE = get_all_targets over the tree; CFR_TGT_ROOT =
+// run_utils.create_target_strategy + encode_options_from_node at the root only
+// (run_utils.py:89-109; generate_test_data.py:18-26), no threshold.
+enum { CFR_TGT_TREE = 0, CFR_TGT_ROOT = 1 };
+
+CIT_HD bool cfr_target_sel(const CfrTree& T, int n, int mode) {
+  return mode == CFR_TGT_ROOT ? T.nodes[n].n_children > 0 : cfr_is_target(T, n);
+}
+CIT_HD int cfr_target_next(const CfrTree& T, int n, int top, int mode) {
+  return mode == CFR_TGT_ROOT ? -1 : cfr_preorder_next(T, n, top);
+}
+
 // Number of targets and of their children (option rows).
-CIT_HD void cfr_count_targets(const CfrTree& T, int root, int32_t& n_targets, int32_t& n_children) {
+CIT_HD void cfr_count_targets(const CfrTree& T, int root, int mode, int32_t& n_targets, int32_t& n_children) {
   n_targets = n_children = 0;
   if (root < 0) return;
-  for (int n = root; n >= 0; n = cfr_preorder_next(T, n))
-    if (cfr_is_target(T, n)) {
+  for (int n = root; n >= 0; n = cfr_target_next(T, n, root, mode))
+    if (cfr_target_sel(T, n, mode)) {
       n_targets++;
       n_children += T.nodes[n].n_children;
     }
@@ -736,12 +749,12 @@ CIT_HD void cfr_count_targets(const CfrTree& T, int root, int32_t& n_targets, in
 //   feat[k][418] = encode_game (role-pick node: player randint(0, 5) of the tree's stream)
 //   value[k][6] = node_value;  regret rows dist[c0 + j] (role-pick: cumulative_regrets[i]),
 //   all ones when they sum to 0;  opt_feat[c0 + j][131] = encode_option of child j.
-CIT_HD void cfr_emit_targets(const CfrTree& T, CitMT& py, int root, int lane, int32_t t0, int32_t c0, int32_t* meta,
-                             float* feat, double* value, double* dist, float* opt_feat) {
+CIT_HD void cfr_emit_targets(const CfrTree& T, CitMT& py, int root, int mode, int lane, int32_t t0, int32_t c0,
+                             int32_t* meta, float* feat, double* value, double* dist, float* opt_feat) {
   if (root < 0) return;
   int32_t t = t0, c = c0;
-  for (int n = root; n >= 0; n = cfr_preorder_next(T, n)) {
-    if (!cfr_is_target(T, n)) continue;
+  for (int n = root; n >= 0; n = cfr_target_next(T, n, root, mode)) {
+    if (!cfr_target_sel(T, n, mode)) continue;
     const CfrNode& N = T.nodes[n];
     const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
     const CfrEdge* E = T.edges + N.first_edge;
@@ -756,7 +769,7 @@ CIT_HD void cfr_emit_targets(const CfrTree& T, CitMT& py, int root, int lane, in
     m[2] = pid;
     m[3] = N.n_children;
     m[4] = c;
-    cit_encode_game(g, feat + (long)t * CIT_FEAT, pid);
+    if (feat) cit_encode_game(g, feat + (long)t * CIT_FEAT, pid);
     for (int k = 0; k < 6; k++) value[(long)t * 6 + k] = N.nv[k];
     bool zero = true;
     for (int j = 0; j < N.n_children; j++) zero = zero && E[j].R[row] == 0.0;

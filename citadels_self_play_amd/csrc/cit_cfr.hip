@@ -121,22 +121,23 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   }
 }
 
-__global__ void k_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, const int32_t* roots,
+__global__ void k_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
                                    int32_t* counts) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= B) return;
   CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
-  cfr_count_targets(T, roots[l], counts[2 * l], counts[2 * l + 1]);
+  cfr_count_targets(T, roots[l], mode, counts[2 * l], counts[2 * l + 1]);
 }
 
-__global__ void k_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, const int32_t* roots, uint32_t* mt,
+__global__ void k_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
+                              uint32_t* mt,
                               uint32_t* idx, const int32_t* offsets, int32_t* meta, float* feat, double* value,
                               double* dist, float* opt_feat) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= B) return;
   CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
   CitMT r = lane_mt(mt, idx, B, l);
-  cfr_emit_targets(T, r, roots[l], (int)l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
+  cfr_emit_targets(T, r, roots[l], mode, (int)l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
   idx[l] = r.pos;
 }
 
@@ -167,20 +168,22 @@ int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt,
   CHECK_LAUNCH();
 }
 
-int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int32_t* counts,
-                         hipStream_t stream) {
-  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !counts) return -1;
+int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
+                         int32_t* counts, hipStream_t stream) {
+  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !counts || mode < 0 || mode > 1) return -1;
   hipLaunchKernelGGL(k_cfr_target_count, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap,
-                     edge_cap, roots, counts);
+                     edge_cap, roots, mode, counts);
   CHECK_LAUNCH();
 }
 
-int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, uint32_t* mt,
+int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode, uint32_t* mt,
                     uint32_t* mt_idx, const int32_t* offsets, int32_t* meta, float* feat, double* value, double* dist,
                     float* opt_feat, hipStream_t stream) {
-  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !mt || !mt_idx || !offsets) return -1;
+  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !mt || !mt_idx || !offsets || mode < 0 ||
+      mode > 1)
+    return -1;
   hipLaunchKernelGGL(k_cfr_targets, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap, edge_cap,
-                     roots, mt, mt_idx, offsets, meta, feat, value, dist, opt_feat);
+                     roots, mode, mt, mt_idx, offsets, meta, feat, value, dist, opt_feat);
   CHECK_LAUNCH();
 }
 

@@ -1703,3 +1703,56 @@ CIT_HD int cit_random_position(CitGame& g, CitMT& rng, uint64_t* seer, uint32_t*
   for (int i = 0; i < W; i++) gw[i] = src[i];
   return n - k;
 }
+
+// create_a_close_to_finished_game(game) (run_utils.py:29-53) on the lane's
+// created game: k = randint(1, max_back); a random playout to the winner with
+// a deep copy before the first and after every step; then, at most `limit`
+// times while the examined game has < 2 options: examine games[-k] (its
+// get_options may mutate it and draw from the stream, as in the reference),
+// k -= 1.  Python indexing: games[-0] is games[0], games[-(-j)] is games[j].
+// `store` holds CIT_CLOSE_ROWS rows: the first `limit` snapshots and a ring of
+// the last max_back (close_slot: a snapshot held in both is always read and
+// written through the ring).  Returns the index of the position (-1 on error).
+#define CIT_CLOSE_LIMIT 100
+#define CIT_CLOSE_BACK 30
+#define CIT_CLOSE_ROWS (CIT_CLOSE_LIMIT + CIT_CLOSE_BACK)
+CIT_HD uint32_t* close_slot(uint32_t* store, int j, int n) {
+  const int W = CIT_GAME_BYTES / 4;
+  if (j >= n - CIT_CLOSE_BACK) return store + (long)(CIT_CLOSE_LIMIT + j % CIT_CLOSE_BACK) * W;
+  return j < CIT_CLOSE_LIMIT ? store + (long)j * W : nullptr;
+}
+CIT_HD int cit_close_position(CitGame& g, CitMT& rng, uint64_t* seer, uint32_t* store) {
+  const int W = CIT_GAME_BYTES / 4;
+  int k = 1 + (int)mt_randbelow(rng, (uint32_t)CIT_CLOSE_BACK);
+  uint32_t* gw = reinterpret_cast<uint32_t*>(&g);
+  int n = 0;
+  for (;;) {                                   // snapshot n, then step
+    if (n < CIT_CLOSE_LIMIT)
+      for (int i = 0; i < W; i++) store[(long)n * W + i] = gw[i];
+    uint32_t* t = store + (long)(CIT_CLOSE_LIMIT + n % CIT_CLOSE_BACK) * W;
+    for (int i = 0; i < W; i++) t[i] = gw[i];
+    n++;
+    if (g.terminal || g.err) break;
+    if (n > CIT_ROLLOUT_CAP) { g.err |= CIT_ERR_STEP_CAP; break; }
+    cit_random_step(g, rng, seer);
+  }
+  if (g.err) return -1;
+  int cnt = 0, limit = 0, idx = -1;
+  while (cnt < 2 && limit < CIT_CLOSE_LIMIT) {
+    int m = k;
+    idx = m > 0 ? n - m : -m;
+    if (idx < 0 || idx >= n) { g.err |= CIT_ERR_INDEX; return -1; }
+    uint32_t* src = close_slot(store, idx, n);
+    if (!src) { g.err |= CIT_ERR_UNSUPPORTED; return -1; }
+    for (int i = 0; i < W; i++) gw[i] = src[i];
+    cit_prepare_options(g, rng, seer);
+    uint32_t e = 0;
+    cnt = cit_count_options(g, e, seer);
+    g.err |= e;
+    for (int i = 0; i < W; i++) src[i] = gw[i];   // the examined snapshot keeps get_options' mutation
+    if (g.err) return -1;
+    k--;
+    limit++;
+  }
+  return idx;
+}

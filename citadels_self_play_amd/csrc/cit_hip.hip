@@ -56,6 +56,14 @@ __global__ void k_mt_draw(uint32_t* mt, uint32_t* idx, int B, int n, uint32_t* o
   idx[l] = r.pos;
 }
 
+__global__ void k_randbelow(uint32_t* mt, uint32_t* idx, int B, uint32_t bound, int32_t* out) {
+  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= B) return;
+  CitMT r = lane_mt(mt, idx, B, l);
+  out[l] = (int32_t)mt_randbelow(r, bound);
+  idx[l] = r.pos;
+}
+
 __global__ void k_init(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int preset) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   long g0 = (long)blockIdx.x * blockDim.x;
@@ -63,7 +71,7 @@ __global__ void k_init(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, cons
   long l = g0 + threadIdx.x;
   if (threadIdx.x < nrows) {
     CitMT r = lane_mt(mt, idx, B, l);
-    mt_seed_cpython(r, seeds[l]);
+    if (seeds) mt_seed_cpython(r, seeds[l]);          // NULL: continue the lane's stream
     CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
     cit_init_game(g, r, preset != 0);
     idx[l] = r.pos;
@@ -207,6 +215,25 @@ __global__ void k_random_position(uint32_t* games, uint32_t* mt, uint32_t* idx, 
   stage_out(lds, games, g0, nrows);
 }
 
+// create_a_close_to_finished_game per lane (generate_test_data positions).
+__global__ void k_close_position(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, uint32_t* store,
+                                 int32_t* index) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  long g0 = (long)blockIdx.x * blockDim.x;
+  int nrows = (int)min((long)blockDim.x, (long)B - g0);
+  stage_in(lds, games, g0, nrows);
+  __syncthreads();
+  if (threadIdx.x < nrows) {
+    long l = g0 + threadIdx.x;
+    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
+    CitMT r = lane_mt(mt, idx, B, l);
+    index[l] = cit_close_position(g, r, seer + l * CIT_SEER_MAX, store + l * (long)CIT_CLOSE_ROWS * ROW_W);
+    idx[l] = r.pos;
+  }
+  __syncthreads();
+  stage_out(lds, games, g0, nrows);
+}
+
 template <class K>
 int set_lds(K kernel, size_t bytes) {
   return (int)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -223,6 +250,7 @@ int ensure_attrs() {
   if (!e) e = set_lds(k_rollout, m);
   if (!e) e = set_lds(k_advance, m);
   if (!e) e = set_lds(k_random_position, m);
+  if (!e) e = set_lds(k_close_position, m);
   if (!e) g_attrs_done = true;
   return e;
 }
@@ -262,9 +290,15 @@ int cit_mt_draw(uint32_t* mt, uint32_t* mt_idx, int B, int n, uint32_t* out, hip
   CHECK_LAUNCH();
 }
 
+int cit_randbelow(uint32_t* mt, uint32_t* mt_idx, int B, int bound, int32_t* out, hipStream_t stream) {
+  if (B <= 0 || bound <= 0 || !mt || !mt_idx || !out) return -1;
+  hipLaunchKernelGGL(k_randbelow, dim3((B + 63) / 64), dim3(64), 0, stream, mt, mt_idx, B, (uint32_t)bound, out);
+  CHECK_LAUNCH();
+}
+
 int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int preset,
              hipStream_t stream) {
-  if (B <= 0 || !games || !mt || !mt_idx || !seeds) return -1;
+  if (B <= 0 || !games || !mt || !mt_idx) return -1;
   if (int e = ensure_attrs()) return e;
   const int G = 64;
   hipLaunchKernelGGL(k_init, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx, B,
@@ -332,6 +366,18 @@ int cit_random_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* s
   const int G = 16;
   hipLaunchKernelGGL(k_random_position, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
                      mt_idx, seer, B, max_move, ring, steps);
+  CHECK_LAUNCH();
+}
+
+int cit_close_rows(void) { return CIT_CLOSE_ROWS; }
+
+int cit_close_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, uint32_t* store,
+                       int32_t* index, hipStream_t stream) {
+  if (B <= 0 || !games || !mt || !mt_idx || !seer || !store || !index) return -1;
+  if (int e = ensure_attrs()) return e;
+  const int G = 16;
+  hipLaunchKernelGGL(k_close_position, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+                     mt_idx, seer, B, store, index);
   CHECK_LAUNCH();
 }
 

@@ -76,7 +76,7 @@ void cith_mt_random(uint32_t* mt, uint32_t* idx, int B, int lane, int n, double*
 void cith_init(CitGame* g, uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int preset) {
   for (int l = 0; l < B; l++) {
     CitMT r = lane_rng(mt, idx, B, l);
-    mt_seed_cpython(r, seeds[l]);
+    if (seeds) mt_seed_cpython(r, seeds[l]);
     cit_init_game(g[l], r, preset != 0);
     SAVE(r);
   }
@@ -263,19 +263,28 @@ void cith_random_position(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* see
   }
 }
 
-void cith_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, const int* roots, int* counts) {
+void cith_close_position(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, uint32_t* store,
+                         int* index) {
   for (int l = 0; l < B; l++) {
-    CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
-    cfr_count_targets(T, roots[l], counts[2 * l], counts[2 * l + 1]);
+    CitMT r = lane_rng(mt, idx, B, l);
+    index[l] = cit_close_position(g[l], r, seer + (long)l * CIT_SEER_MAX, store);
+    SAVE(r);
   }
 }
 
-void cith_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, const int* roots, uint32_t* mt, uint32_t* idx,
-                      const int* offsets, int* meta, float* feat, double* value, double* dist, float* opt_feat) {
+void cith_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, const int* roots, int mode, int* counts) {
+  for (int l = 0; l < B; l++) {
+    CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+    cfr_count_targets(T, roots[l], mode, counts[2 * l], counts[2 * l + 1]);
+  }
+}
+
+void cith_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, const int* roots, int mode, uint32_t* mt,
+                      uint32_t* idx, const int* offsets, int* meta, float* feat, double* value, double* dist, float* opt_feat) {
   for (int l = 0; l < B; l++) {
     CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
     CitMT r = lane_rng(mt, idx, B, l);
-    cfr_emit_targets(T, r, roots[l], l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
+    cfr_emit_targets(T, r, roots[l], mode, l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
     SAVE(r);
   }
 }

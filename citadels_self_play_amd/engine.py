@@ -58,6 +58,23 @@ class GameBatch:
         self.winner = torch.full((self.B,), -1, dtype=torch.int32, device=d)
         self.reset()
 
+    @classmethod
+    def from_tensors(cls, games, mt, mt_idx, seer, np_mt=None, np_idx=None):
+        """A batch over existing device state (no init): games [B,1456] u8, mt [624,B],
+        mt_idx [B], seer [B,SEER_MAX] and optionally numpy streams np_mt/np_idx."""
+        self = cls.__new__(cls)
+        self.lib = _lib.load()
+        self.device = games.device
+        self.B = int(games.shape[0])
+        self.preset = True
+        self.games_per_block = 0
+        self.games, self.mt, self.mt_idx, self.seer = games, mt, mt_idx, seer
+        if np_mt is not None:
+            self.np_mt, self.np_idx = np_mt, np_idx
+        self.steps = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self.winner = torch.full((self.B,), -1, dtype=torch.int32, device=self.device)
+        return self
+
     def reset(self):
         """Re-create every lane's game from its seed (cit_init)."""
         _lib.check(self.lib.cit_init(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), self.B, _ptr(self.seeds),
@@ -145,7 +162,18 @@ class GameBatch:
         del ring
         return steps
 
-    def cfr_targets(self, roots):
+    def close_position(self):
+        """create_a_close_to_finished_game (run_utils.py:29-53) on every lane's created
+        game.  Returns the snapshot index of each position (-1 on a lane error)."""
+        d = self.device
+        store = torch.empty(self.B * self.lib.cit_close_rows() * L.GAME_BYTES, dtype=torch.uint8, device=d)
+        index = torch.zeros(self.B, dtype=torch.int32, device=d)
+        _lib.check(self.lib.cit_close_position(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.seer),
+                                               self.B, _ptr(store), _ptr(index), _stream()), "cit_close_position")
+        del store
+        return index
+
+    def cfr_targets(self, roots, mode=0):
         """get_all_targets over the trees of the last cfr_decide (roots = stats[:, 0]).
         Returns a dict: meta [n,5] (lane, node, player override, n_children, first
         option row), feat [n,418] f32, value [n,6] f64, dist [m] f64, opt_feat [m,131]
@@ -154,7 +182,7 @@ class GameBatch:
         roots = roots.to(device=d, dtype=torch.int32).contiguous()
         counts = torch.zeros((self.B, 2), dtype=torch.int32, device=d)
         _lib.check(self.lib.cit_cfr_target_count(_ptr(self.pool), self.B, self.node_cap, self.edge_cap, _ptr(roots),
-                                                 _ptr(counts), _stream()), "cit_cfr_target_count")
+                                                 int(mode), _ptr(counts), _stream()), "cit_cfr_target_count")
         offs = torch.zeros_like(counts)
         offs[1:] = torch.cumsum(counts, dim=0)[:-1]
         tot = counts.sum(dim=0).cpu()
@@ -165,7 +193,7 @@ class GameBatch:
                "dist": torch.zeros(nc, dtype=torch.float64, device=d),
                "opt_feat": torch.zeros((nc, 131), dtype=torch.float32, device=d), "counts": counts}
         _lib.check(self.lib.cit_cfr_targets(_ptr(self.pool), self.B, self.node_cap, self.edge_cap, _ptr(roots),
-                                            _ptr(self.mt), _ptr(self.mt_idx), _ptr(offs), _ptr(out["meta"]),
+                                            int(mode), _ptr(self.mt), _ptr(self.mt_idx), _ptr(offs), _ptr(out["meta"]),
                                             _ptr(out["feat"]), _ptr(out["value"]), _ptr(out["dist"]),
                                             _ptr(out["opt_feat"]), _stream()), "cit_cfr_targets")
         return out

@@ -1,0 +1,139 @@
+"""Batched self-play drivers over the device engine (one process per GPU).
+
+The reference fans games out over `multiprocessing.Pool` workers, each
+running one game through the Python object API (train_from_scratch.py:39-42,
+compare_to_random.py:40-42, generate_test_data.py:28-31).  Here one rank owns
+a contiguous block of the global games (seeded by global index, so results
+do not depend on the world size) and runs them as one batch on its GPU:
+
+* `decide`        - configs 3/4: positions `random.randint(lo, hi)` random steps
+                    into create_game(), one run_mccfr decision each (cfr_train
+                    without a model, cfr_pred with the value net).
+* `simulate_games`- config 5 / simulate_game (train_from_scratch.py:23-36):
+                    create_a_random_game(100) -> cfr_train(M) (+ live choice) ->
+                    get_all_targets.
+* `setup_games`   - generate_test_data.setup_game (generate_test_data.py:9-26).
+* `all_gather_targets` - the only data-path collective: pools the (encode_game,
+                    node_value) pairs of all ranks (replaces Pool.starmap's
+                    result pooling); two RCCL all_gathers (counts, packed rows).
+* `broadcast_model`    - rank 0's value-net parameters to every rank, once.
+
+All device work goes through libcitadels_hip.so (engine.GameBatch); nothing
+here falls back to the CPU.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .engine import GameBatch
+
+TARGET_ROW_BYTES = 418 * 4 + 6 * 8      # encode_game f32[418] | node_value f64[6]
+
+
+def world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard(n_total, base_seed=0, rank=None, world_size=None):
+    """Global game indices [rank*n/P, (rank+1)*n/P) -> their seeds."""
+    r, w = world()
+    rank = r if rank is None else rank
+    world_size = w if world_size is None else world_size
+    lo = n_total * rank // world_size
+    hi = n_total * (rank + 1) // world_size
+    return np.arange(base_seed + lo, base_seed + hi, dtype=np.int64)
+
+
+def broadcast_model(model, src=0):
+    """dist.broadcast of every parameter / buffer of `model` (in place)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return model
+    for t in list(model.parameters()) + list(model.buffers()):
+        dist.broadcast(t.data, src)
+    return model
+
+
+def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None):
+    """Configs 3/4 (tools/gen_golden_cfr.py harness): per seed s, random.seed(s),
+    np.random.seed(s), create_game(), randint(lo, hi) random steps, then
+    run_mccfr(game, net, iters).  Returns (batch, chosen, stats[, rounds])."""
+    b = GameBatch(seeds, preset=True, device=device)
+    b.advance_random(lo, hi)
+    b.seed_numpy()
+    if net is None:
+        chosen, stats = b.cfr_decide(iters, node_cap=node_cap or 1024)
+        return b, chosen, stats, 0
+    chosen, stats, rounds = b.cfr_pred(iters, net, max_depth=10, node_cap=node_cap or 2048)
+    return b, chosen, stats, rounds
+
+
+def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None):
+    """simulate_game (train_from_scratch.py:23-36, pretrain / training=True: the
+    search ignores the model) for every seed: random.seed(s), np.random.seed(s),
+    create_a_random_game(max_move), run_mccfr(iters, training=True),
+    get_all_targets.  Returns (batch, stats, targets dict of device tensors)."""
+    b = GameBatch(seeds, preset=True, device=device)
+    b.random_position(max_move)
+    b.seed_numpy()
+    cap = node_cap or max(1024, 4 * iters)
+    chosen, stats = b.cfr_decide(iters, node_cap=cap)
+    targets = b.cfr_targets(stats[:, 0], mode=0)
+    return b, stats, targets
+
+
+def setup_games(seeds, iters, node_cap=None, device=None):
+    """generate_test_data.setup_game for every seed: random.seed(s), np.random.seed(s),
+    create_game(), create_a_close_to_finished_game, encode_game, run_mccfr(iters),
+    encode_options_from_node + create_target_strategy at the root.  Lanes whose
+    search raised ValueError (terminal positions) yield no tuple, as setup_game
+    returns [].  Returns (batch, feat [B,418], stats, root targets)."""
+    from . import _lib
+    b = GameBatch(seeds, preset=True, device=device)
+    b.close_position()
+    feat = torch.zeros((b.B, 418), dtype=torch.float32, device=b.device)
+    _lib.check(b.lib.cit_encode_games(b.games.data_ptr(), b.B, -1, feat.data_ptr(),
+                                      torch.cuda.current_stream(b.device).cuda_stream), "cit_encode_games")
+    b.seed_numpy()
+    chosen, stats = b.cfr_decide(iters, node_cap=node_cap or max(1024, 4 * iters))
+    targets = b.cfr_targets(stats[:, 0], mode=1)
+    return b, feat, stats, targets
+
+
+def pack_targets(feat, value):
+    """[n,418] f32 + [n,6] f64 -> [n, TARGET_ROW_BYTES] uint8 rows."""
+    n = feat.shape[0]
+    f = feat.contiguous().view(torch.uint8).reshape(n, 418 * 4)
+    v = value.contiguous().view(torch.uint8).reshape(n, 6 * 8)
+    return torch.cat([f, v], dim=1)
+
+
+def unpack_targets(rows):
+    n = rows.shape[0]
+    f = rows[:, :418 * 4].contiguous().view(torch.float32).reshape(n, 418)
+    v = rows[:, 418 * 4:].contiguous().view(torch.float64).reshape(n, 6)
+    return f, v
+
+
+def all_gather_targets(feat, value, group=None):
+    """Pool every rank's (encode_game, node_value) target pairs on every rank,
+    in rank order: all_gather of the int64 counts, then of the rows padded to
+    the largest count.  Works on any backend (RCCL on device tensors, gloo on
+    CPU tensors)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return feat, value
+    ws = dist.get_world_size(group)
+    dev = feat.device
+    n = torch.tensor([feat.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(ws)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts)
+    rows = torch.zeros((m, TARGET_ROW_BYTES), dtype=torch.uint8, device=dev)
+    if feat.shape[0]:
+        rows[:feat.shape[0]] = pack_targets(feat, value)
+    bufs = [torch.empty_like(rows) for _ in range(ws)]
+    dist.all_gather(bufs, rows, group=group)
+    pooled = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+    return unpack_targets(pooled)

@@ -60,10 +60,14 @@ int cit_mt_seed(uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, in
 /* n raw 32-bit outputs of every lane's stream into out[B][n] (RNG parity tests). */
 int cit_mt_draw(uint32_t* mt, uint32_t* mt_idx, int B, int n, uint32_t* out, hipStream_t stream);
 
+/* random.randrange(bound) (_randbelow) from every lane's stream into out[l]. */
+int cit_randbelow(uint32_t* mt, uint32_t* mt_idx, int B, int bound, int32_t* out, hipStream_t stream);
+
 /* Game(preset) + create_game's setup_round for every lane, with the lane's
  * stream freshly seeded from seeds[l]: replaces `random.seed(s); create_game()`
  * (run_utils.py:20-27, game/game.py:17-24,420-540,144-171).  preset=0 builds
- * the random-role Game() (game.py:491-520). */
+ * the random-role Game() (game.py:491-520).  seeds == NULL continues each
+ * lane's current stream instead (create_game() without a reseed). */
 int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int preset,
              hipStream_t stream);
 
@@ -168,18 +172,33 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
 int cit_random_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_move,
                         uint32_t* ring, int32_t* steps, hipStream_t stream);
 
+/* create_a_close_to_finished_game(game) (run_utils.py:29-53) on every lane's
+ * created game (cit_init: create_game, same stream): k = randint(1, 30), a
+ * random playout to the winner, then games[-k], games[-(k-1)], ... (Python
+ * indexing) examined with get_options until one has >= 2 options (at most
+ * 100).  `store`: B * cit_close_rows() * cit_game_bytes() bytes of scratch.
+ * index[l] = snapshot index of the position, -1 on error. */
+int cit_close_rows(void);
+int cit_close_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, uint32_t* store,
+                       int32_t* index, hipStream_t stream);
+
 /* get_all_targets (deep_mccfr.py:258-274) / build_train_targets (:321-345)
- * over the finished trees of cit_cfr_decide (same pool, roots = stats[:,0]).
+ * over the finished trees of cit_cfr_decide (same pool, roots = stats[:,0];
+ * any node id gives that node's subtree, as node.get_all_targets does).
  * Threshold: build_train_targets' default 15 (get_all_targets does not pass
  * its own).  Pass 1: counts[l] = {targets, option rows}.  Pass 2 (exclusive
  * prefix sums of counts as offsets): per target k, meta[k] = {lane, node,
  * player override (-1 none), n_children, first option row}, feat[k][418]
  * (encode_game; a role-pick node draws randint(0,5) from the lane's CPython
  * stream), value[k][6] = node_value (f64), dist[row] = regret target (f64),
- * opt_feat[row][131] = encode_option of each child, rows in child order. */
-int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int32_t* counts,
-                         hipStream_t stream);
-int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, uint32_t* mt,
+ * opt_feat[row][131] = encode_option of each child, rows in child order.
+ * mode 0: the whole tree (get_all_targets).  mode 1: the root only, no
+ * threshold (run_utils.create_target_strategy + encode_options_from_node,
+ * run_utils.py:89-109, as generate_test_data.py:18-26 uses them); feat may be
+ * NULL (generate_test_data encodes the position before the search). */
+int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
+                         int32_t* counts, hipStream_t stream);
+int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode, uint32_t* mt,
                     uint32_t* mt_idx, const int32_t* offsets, int32_t* meta, float* feat, double* value, double* dist,
                     float* opt_feat, hipStream_t stream);
 

@@ -481,3 +481,55 @@ def simulate_game(seed, iters, max_move=100):
     pos = clone(g)
     chosen, tr = run_mccfr(g, npr, iters, training=True)
     return pos, chosen, tr, get_all_targets(tr.root, g.rng)
+
+
+# --------------------------------------------------- generate_test_data
+def close_position(g, max_back=30):
+    """create_a_close_to_finished_game(game) (run_utils.py:29-53): plays `g` to
+    the end (deep copy before the first and after every step), then examines
+    games[-k] for k = randint(1, max_back), k-1, ... (Python indexing, so k <= 0
+    wraps to the front) until one has >= 2 options, at most 100 times."""
+    rng = g.rng
+    k = rng.randint(1, max_back)
+    games = [clone(g)]
+    while True:
+        opts = g.get_options()
+        w = g.carry_out(opts[rng._randbelow(len(opts))])
+        games.append(clone(g))
+        if w is not None:
+            break
+    opts, limit, pos = [], 0, None
+    while len(opts) < 2 and limit < 100:
+        pos = games[-k]
+        opts = pos.get_options()
+        k -= 1
+        limit += 1
+    return pos
+
+
+def setup_game(seed, iters):
+    """generate_test_data.setup_game (generate_test_data.py:9-31) after
+    random.seed(seed), np.random.seed(seed), with run_mccfr(max_iterations=iters).
+    Returns (position, result) where result is "ValueError", "empty" or
+    (encode_game, options [nch,131], node_value, target) (create_target_strategy,
+    run_utils.py:98-109), and the tree (or None)."""
+    import mlp_oracle as M
+    g = O.new_game(seed, True)
+    npr = np.random.RandomState(seed)
+    pos = close_position(g)
+    snap = clone(pos)
+    x = M.encode_game(pos)
+    try:
+        _, tr = run_mccfr(pos, npr, iters)
+    except ValueError:
+        return snap, "ValueError", None
+    root = tr.root
+    opts = np.stack([M.encode_option(o) for o, _ in root.children]) if root.children else None
+    if len(root.R) == 0:
+        return snap, "empty", tr
+    R = np.array(root.R, dtype=np.float64)
+    if R.shape == (6, 10):
+        R = R[pos.rng.randint(0, 5)]
+    if R.sum() == 0:
+        R = np.ones_like(R)
+    return snap, (x, opts, root.nv.copy(), R), tr

@@ -21,7 +21,7 @@ def build(force=False):
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(s) for s in srcs):
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", srcs[0], "-o", LIB])
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-strict-aliasing", "-shared", "-fPIC", srcs[0], "-o", LIB])
     return LIB
 
 
@@ -177,13 +177,31 @@ def random_position(hb, max_move=100):
     return steps
 
 
-def cfr_targets(cf, roots):
+def close_position(hb):
+    """create_a_close_to_finished_game on every lane's created game."""
+    store = np.zeros(130 * L.GAME_BYTES // 4, np.uint32)
+    index = np.zeros(hb.B, np.int32)
+    lib().cith_close_position(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(hb.seer), C.c_int(hb.B), _p(store), _p(index))
+    return index
+
+
+def cfr_root_target(cf, roots):
+    """create_target_strategy + encode_options_from_node at each lane's root ->
+    per lane (None, options, node_value, target) or None."""
+    t = cfr_targets(cf, roots, mode=1)
+    out = [None] * cf.hb.B
+    for k, (lane, node, pid, nch, c0) in enumerate(t["meta"]):
+        out[lane] = (None, t["opt_feat"][c0:c0 + nch], t["value"][k], t["dist"][c0:c0 + nch])
+    return out
+
+
+def cfr_targets(cf, roots, mode=0):
     """get_all_targets over every lane's finished tree -> dict of arrays (see cfr_emit_targets)."""
     hb = cf.hb
     roots = np.ascontiguousarray(roots, np.int32)
     counts = np.zeros((hb.B, 2), np.int32)
     lib().cith_cfr_target_count(_p(cf.pool), C.c_int(hb.B), C.c_int(cf.node_cap), C.c_int(cf.edge_cap), _p(roots),
-                                _p(counts))
+                                C.c_int(mode), _p(counts))
     offs = np.zeros_like(counts)
     offs[1:] = np.cumsum(counts, axis=0)[:-1]
     nt, nc = int(counts[:, 0].sum()), int(counts[:, 1].sum())
@@ -191,7 +209,7 @@ def cfr_targets(cf, roots):
            "value": np.zeros((nt, 6), np.float64), "dist": np.zeros(nc, np.float64),
            "opt_feat": np.zeros((nc, 131), np.float32), "counts": counts}
     lib().cith_cfr_targets(_p(cf.pool), C.c_int(hb.B), C.c_int(cf.node_cap), C.c_int(cf.edge_cap), _p(roots),
-                           _p(hb.mt), _p(hb.idx), _p(offs), _p(out["meta"]), _p(out["feat"]), _p(out["value"]),
+                           C.c_int(mode), _p(hb.mt), _p(hb.idx), _p(offs), _p(out["meta"]), _p(out["feat"]), _p(out["value"]),
                            _p(out["dist"]), _p(out["opt_feat"]))
     return out
 

@@ -39,3 +39,15 @@ def test_bad_args_rejected(lib):
     # argument validation happens before any launch: no GPU is touched
     assert lib.cit_rollout_random(None, None, None, None, 0, -1, 0, None, None, None) == -1
     assert lib.cit_init(None, None, None, 4, None, 1, None) == -1
+
+
+def test_api_error_mapping():
+    import pytest
+    from citadels_self_play_amd import api
+    with pytest.raises(IndexError):
+        api.raise_for(0x2)
+    with pytest.raises(ValueError):
+        api.raise_for(0x8)
+    with pytest.raises(KeyError):
+        api.raise_for(0x4)
+    api.raise_for(0)

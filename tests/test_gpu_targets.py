@@ -73,3 +73,31 @@ def test_gpu_targets_batch_invariance():
         for x, y in zip(a, bb):
             for u, v in zip(x, y):
                 assert np.array_equal(u, v)
+
+
+def test_gpu_setup_game_golden():
+    """generate_test_data.setup_game (500 iterations) on the device vs the reference."""
+    from citadels_self_play_amd import _lib
+    from citadels_self_play_amd.engine import GameBatch
+    recs = load_golden("testdata500.json.gz")
+    b = GameBatch([r["seed"] for r in recs], preset=True)
+    index = b.close_position().cpu().numpy()
+    assert (index >= 0).all()
+    rows = b.rows()
+    for l, r in enumerate(recs):
+        assert canon.canon_game(L.game_from_bytes(rows[l])) == r["position"], r["seed"]
+    feat = torch.zeros((b.B, 418), dtype=torch.float32, device=b.device)
+    _lib.check(b.lib.cit_encode_games(b.games.data_ptr(), b.B, -1, feat.data_ptr(), None), "encode")
+    b.seed_numpy()
+    chosen, stats = b.cfr_decide(recs[0]["iters"], node_cap=4096)
+    t = {k: v.cpu().numpy() for k, v in b.cfr_targets(stats[:, 0], mode=1).items()}
+    feat, stats = feat.cpu().numpy(), stats.cpu().numpy()
+    by_lane = {int(m[0]): (k, m) for k, m in enumerate(t["meta"])}
+    for l, r in enumerate(recs):
+        if r["result"] == "ValueError":
+            assert stats[l][4] != 0 and l not in by_lane, r["seed"]
+            continue
+        assert stats[l][4] == 0 and stats[l][1] == r["nodes"] and stats[l][3] == r["carry_outs"], r["seed"]
+        k, (lane, node, pid, nch, c0) = by_lane[l]
+        check_targets([(feat[l], t["opt_feat"][c0:c0 + nch], t["value"][k], t["dist"][c0:c0 + nch])],
+                      [r["result"]], r["seed"])

@@ -37,6 +37,7 @@ _SIGS = {
     "cit_cfr_decide": ([vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, vp], i32),
     "cit_cfr_state_bytes": ([], i32),
     "cit_randbelow": ([vp, vp, i32, i32, vp, vp], i32),
+    "cit_advance_policy": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
     "cit_random_position": ([vp, vp, vp, vp, i32, i32, vp, vp, vp], i32),
     "cit_cfr_target_count": ([vp, i32, i32, i32, vp, i32, vp, vp], i32),
     "cit_cfr_targets": ([vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),

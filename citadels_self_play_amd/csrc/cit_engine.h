@@ -1675,6 +1675,37 @@ CIT_HD int cit_random_step(CitGame& g, CitMT& rng, uint64_t* seer) {
   return (w >= 0 || g.err || g.terminal) ? 1 : 0;
 }
 
+// compare_to_random.play_games' step loop (compare_to_random.py:16-35) up to
+// the next searched decision.  Seats in `search_mask` decide by search when
+// they have more than one option; that test is one get_options call, and a
+// searched seat with <= 1 option falls through to the else branch, which calls
+// get_options again before random.choice.  Other seats make one call.
+// Returns the deciding seat, -1 when the game is over (or max_steps random
+// steps were taken), -2 on a lane error.
+CIT_HD int cit_advance_policy(CitGame& g, CitMT& rng, uint64_t* seer, int search_mask, int max_steps, int& steps) {
+  int s = 0;
+  while (!g.terminal && !g.err && s < max_steps) {
+    int pid = g.gs_pid;
+    uint32_t e = 0;
+    cit_prepare_options(g, rng, seer);
+    int n = cit_count_options(g, e, seer);
+    if (e) { g.err |= e; break; }
+    if (pid >= 0 && ((search_mask >> pid) & 1)) {
+      if (n > 1) { steps += s; return pid; }
+      cit_prepare_options(g, rng, seer);
+      n = cit_count_options(g, e, seer);
+      if (e) { g.err |= e; break; }
+    }
+    if (n == 0) { g.err |= CIT_ERR_EMPTY; break; }
+    int k = (int)mt_randbelow(rng, (uint32_t)n);
+    CitOpt o = cit_pick_option(g, k, seer);
+    cit_carry_out(g, o, rng);
+    s++;
+  }
+  steps += s;
+  return g.err ? -2 : -1;
+}
+
 // create_a_random_game(max_move) (run_utils.py:55-73) on a lane whose CPython
 // stream is already seeded: k = randint(1, max_move); create_game(); a random
 // playout to the winner keeping the game after every step (deepcopy ->

@@ -198,6 +198,27 @@ __global__ void k_advance(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t
   stage_out(lds, games, g0, nrows);
 }
 
+// compare_to_random's step loop to the next searched decision per lane.
+__global__ void k_advance_policy(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int search_mask,
+                                 int max_steps, int32_t* status, int32_t* steps_out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  long g0 = (long)blockIdx.x * blockDim.x;
+  int nrows = (int)min((long)blockDim.x, (long)B - g0);
+  stage_in(lds, games, g0, nrows);
+  __syncthreads();
+  if (threadIdx.x < nrows) {
+    long l = g0 + threadIdx.x;
+    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
+    CitMT r = lane_mt(mt, idx, B, l);
+    int st = steps_out[l];
+    status[l] = cit_advance_policy(g, r, seer + l * CIT_SEER_MAX, search_mask, max_steps, st);
+    steps_out[l] = st;
+    idx[l] = r.pos;
+  }
+  __syncthreads();
+  stage_out(lds, games, g0, nrows);
+}
+
 // create_a_random_game(max_move) per lane (train_from_scratch data generation).
 __global__ void k_random_position(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_move,
                                   uint32_t* ring, int32_t* steps_out) {
@@ -251,6 +272,7 @@ int ensure_attrs() {
   if (!e) e = set_lds(k_advance, m);
   if (!e) e = set_lds(k_random_position, m);
   if (!e) e = set_lds(k_close_position, m);
+  if (!e) e = set_lds(k_advance_policy, m);
   if (!e) g_attrs_done = true;
   return e;
 }
@@ -378,6 +400,16 @@ int cit_close_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
   const int G = 16;
   hipLaunchKernelGGL(k_close_position, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
                      mt_idx, seer, B, store, index);
+  CHECK_LAUNCH();
+}
+
+int cit_advance_policy(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int search_mask,
+                       int max_steps, int32_t* status, int32_t* steps, hipStream_t stream) {
+  if (B <= 0 || !games || !mt || !mt_idx || !seer || !status || !steps) return -1;
+  if (int e = ensure_attrs()) return e;
+  const int G = 1;
+  hipLaunchKernelGGL(k_advance_policy, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+                     mt_idx, seer, B, search_mask, max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps, status, steps);
   CHECK_LAUNCH();
 }
 

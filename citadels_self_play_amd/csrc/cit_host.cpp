@@ -254,6 +254,16 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
   return waiting;
 }
 
+void cith_advance_policy(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int search_mask,
+                         int max_steps, int* status, int* steps) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    status[l] = cit_advance_policy(g[l], r, seer + (long)l * CIT_SEER_MAX, search_mask,
+                                   max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps, steps[l]);
+    SAVE(r);
+  }
+}
+
 void cith_random_position(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_move,
                           uint32_t* ring, int* steps) {
   for (int l = 0; l < B; l++) {

@@ -147,6 +147,37 @@ class GameBatch:
                                            _stream()), "cit_cfr_decide")
         return chosen, stats
 
+    def advance_policy(self, search_mask=0b11, max_steps=-1):
+        """compare_to_random's step loop up to each lane's next searched decision
+        (cit_advance_policy).  Returns status [B] (seat to decide, -1 over, -2 error)."""
+        status = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_advance_policy(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.seer),
+                                               self.B, int(search_mask), int(max_steps), _ptr(status),
+                                               _ptr(self.steps), _stream()), "cit_advance_policy")
+        return status
+
+    def subset(self, lanes):
+        """A new batch holding copies of `lanes` (rows, both streams, seer scratch)."""
+        lanes = torch.as_tensor(lanes, dtype=torch.long, device=self.device)
+        sub = GameBatch.from_tensors(self.games[lanes].contiguous(), self.mt[:, lanes].contiguous(),
+                                     self.mt_idx[lanes].contiguous(), self.seer[lanes].contiguous(),
+                                     self.np_mt[:, lanes].contiguous() if hasattr(self, "np_mt") else None,
+                                     self.np_idx[lanes].contiguous() if hasattr(self, "np_idx") else None)
+        sub.steps = self.steps[lanes].contiguous()
+        return sub
+
+    def scatter(self, sub, lanes):
+        """Write a subset batch back into `lanes`."""
+        lanes = torch.as_tensor(lanes, dtype=torch.long, device=self.device)
+        self.games[lanes] = sub.games
+        self.mt[:, lanes] = sub.mt
+        self.mt_idx[lanes] = sub.mt_idx
+        self.seer[lanes] = sub.seer
+        self.steps[lanes] = sub.steps
+        if hasattr(sub, "np_mt"):
+            self.np_mt[:, lanes] = sub.np_mt
+            self.np_idx[lanes] = sub.np_idx
+
     def random_position(self, max_move=100, seeds=None):
         """random.seed(seed); create_a_random_game(max_move) (run_utils.py:55-73) on every
         lane.  Returns steps into the game of each position (-1 on a lane error)."""

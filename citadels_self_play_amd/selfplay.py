@@ -21,6 +21,8 @@ do not depend on the world size) and runs them as one batch on its GPU:
 All device work goes through libcitadels_hip.so (engine.GameBatch); nothing
 here falls back to the CPU.
 """
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -28,6 +30,18 @@ import torch.distributed as dist
 from .engine import GameBatch
 
 TARGET_ROW_BYTES = 418 * 4 + 6 * 8      # encode_game f32[418] | node_value f64[6]
+
+
+def init_distributed():
+    """One process per GPU under torchrun (RANK / LOCAL_RANK / WORLD_SIZE); RCCL
+    ("nccl") process group when WORLD_SIZE > 1.  Returns (rank, world, device)."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if ws > 1 and not dist.is_initialized():
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    r, w = world()
+    return r, w, torch.device("cuda", local)
 
 
 def world():
@@ -137,3 +151,28 @@ def all_gather_targets(feat, value, group=None):
     dist.all_gather(bufs, rows, group=group)
     pooled = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
     return unpack_targets(pooled)
+
+
+def targets_to_tuples(t, feat=None):
+    """The reference's target tuples (deep_mccfr.py:321-345 / generate_test_data.py:26)
+    from a cfr_targets dict: (encode_game f32[418], options f32[1,nch,131],
+    node_value f64[6], regret target f64[nch]) per target, CPU tensors, in
+    target order.  `feat` [B,418] overrides the per-target encode rows by lane
+    (generate_test_data encodes the position before the search)."""
+    h = {k: v.cpu() for k, v in t.items()}
+    fx = feat.cpu() if feat is not None else None
+    out = []
+    for k, (lane, node, pid, nch, c0) in enumerate(h["meta"].tolist()):
+        x = fx[lane].clone() if fx is not None else h["feat"][k].clone()
+        out.append((x, h["opt_feat"][c0:c0 + nch].clone().unsqueeze(0), h["value"][k].clone(),
+                    h["dist"][c0:c0 + nch].clone()))
+    return out
+
+
+def all_gather_objects(obj, group=None):
+    """Pool a picklable per-rank list on every rank (rank order)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return list(obj)
+    bufs = [None] * dist.get_world_size(group)
+    dist.all_gather_object(bufs, obj, group=group)
+    return [x for b in bufs for x in b]

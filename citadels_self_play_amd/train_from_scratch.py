@@ -1,0 +1,105 @@
+"""train_from_scratch (train_from_scratch.py:23-111) on the device engine, one
+process per GPU:
+
+    torchrun --nproc-per-node 8 -m citadels_self_play_amd.train_from_scratch --iters 200000
+
+Each data round, every rank runs `--games-per-gpu` simulate_game trees
+(create_a_random_game(100) -> cfr_train(iters, training=True) ->
+get_all_targets) as one batch (selfplay.simulate_games); the (encode_game,
+node_value) pairs are pooled across ranks with an RCCL all-gather until
+`--min-targets` are collected (get_mccfr_targets, :45-63).  Rank 0 trains the
+value net (train.train_node_value_only) and the weights are broadcast.  The
+full target tuples are written per rank in the reference's pickle layout
+(list of (x, options, node_value, target) tensors).  The model passed to the
+search in the training phases does not change the search (training=True uses
+no predictions, deep_mccfr.py:119-126,279), so every phase runs the same
+device search.
+"""
+import argparse
+import os
+import pickle
+import time
+
+import torch
+
+from . import selfplay
+from .models import ValueOnlyNN
+
+
+def collect(rank, world, args, phase, min_targets, log):
+    feats, values, tuples = [], [], []
+    pooled = 0
+    rnd = 0
+    while pooled < min_targets:
+        base = args.seed + (phase * 1000 + rnd) * args.games_per_gpu * world
+        seeds = selfplay.shard(args.games_per_gpu * world, base_seed=base)
+        t0 = time.time()
+        b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap)
+        f, v = selfplay.all_gather_targets(t["feat"], t["value"])
+        feats.append(f.cpu())
+        values.append(v.cpu())
+        if args.save_tuples:
+            tuples += selfplay.targets_to_tuples(t)
+        pooled += f.shape[0]
+        errs = int((stats[:, 4] != 0).sum())
+        log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), %d lanes with errors, %.1fs"
+            % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, errs, time.time() - t0))
+        rnd += 1
+    return torch.cat(feats), torch.cat(values), tuples
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=200000)
+    ap.add_argument("--games-per-gpu", type=int, default=64)
+    ap.add_argument("--node-cap", type=int, default=None)
+    ap.add_argument("--pretrain-targets", type=int, default=20000)
+    ap.add_argument("--train-targets", type=int, default=5000)
+    ap.add_argument("--phases", type=int, default=5)
+    ap.add_argument("--epochs", type=int, default=1000)
+    ap.add_argument("--batch-size", type=int, default=2048)
+    ap.add_argument("--val", default="validation_targets.pkl", help="generate_test_data output")
+    ap.add_argument("--out", default=".")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--save-tuples", action="store_true")
+    args = ap.parse_args(argv)
+    rank, world, dev = selfplay.init_distributed()
+
+    def log(msg):
+        if rank == 0:
+            print(msg, flush=True)
+
+    if os.path.exists(args.val):
+        with open(args.val, "rb") as f:          # this framework's own generate_test_data output
+            val = pickle.load(f)
+    else:
+        log("no %s: building a validation set with generate_test_data.setup_games" % args.val)
+        seeds = selfplay.shard(max(64, args.games_per_gpu) * world, base_seed=10 ** 9 + args.seed)
+        b, feat, stats, t = selfplay.setup_games(seeds, min(args.iters, 20000))
+        val = selfplay.all_gather_objects(selfplay.targets_to_tuples(t, feat))
+    plan = [("pretrain", args.pretrain_targets, 0.3703517140136571)] + \
+        [("train%d" % u, args.train_targets, 0.02) for u in range(args.phases)]
+    model = ValueOnlyNN(418, 512)
+    for phase, (name, need, lr) in enumerate(plan):
+        folder = os.path.join(args.out, name)
+        feat, value, tuples = collect(rank, world, args, phase, need, log)
+        if args.save_tuples:
+            os.makedirs(folder, exist_ok=True)
+            with open(os.path.join(folder, "targets_rank%d.pkl" % rank), "wb") as f:
+                pickle.dump(tuples, f)
+        if rank == 0:
+            best, model, _ = selfplay_train(feat, value, val, args, lr, folder, dev)
+            log("%s: %d targets, best eval loss %.5f" % (name, feat.shape[0], best))
+        model = selfplay.broadcast_model(model.to(dev))
+    return model
+
+
+def selfplay_train(feat, value, val, args, lr, folder, dev):
+    from .train import train_node_value_only
+    return train_node_value_only((feat, value), val, epochs=args.epochs, lr=lr, hidden_size=512,
+                                 gamma=0.8851980333411889, batch_size=args.batch_size, device=dev,
+                                 parent_folder=folder)
+
+
+if __name__ == "__main__":
+    main()

@@ -160,6 +160,18 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
                       void* state, const float* probs, float* feat, CitOption* chosen, int32_t* waiting,
                       hipStream_t stream);
 
+/* compare_to_random.play_games' step loop (compare_to_random.py:16-35) on
+ * every lane up to its next searched decision: seats in search_mask (bit p =
+ * seat p; the reference searches for seats 0 and 1) decide by search when they
+ * have more than one option, the others play random.choice, with the
+ * reference's exact sequence of get_options calls.  status[l] = the seat to
+ * decide next, -1 game over (or max_steps random steps; <0 = no cap), -2
+ * error; steps[l] += random steps taken.  The caller runs the search for the
+ * stopped lanes (cit_cfr_decide / cit_cfr_pred_step), applies cit_carry_out of
+ * the chosen option and calls again. */
+int cit_advance_policy(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int search_mask,
+                       int max_steps, int32_t* status, int32_t* steps, hipStream_t stream);
+
 /* ---- training-data generation (train_from_scratch.py:23-36 simulate_game) ---- */
 
 /* create_a_random_game(max_move) (run_utils.py:55-73) on every lane, whose

@@ -533,3 +533,32 @@ def setup_game(seed, iters):
     if R.sum() == 0:
         R = np.ones_like(R)
     return snap, (x, opts, root.nv.copy(), R), tr
+
+
+# ---------------------------------------------------- compare_to_random
+def compare_game(seed, model, pred_iters=200, train_iters=2000):
+    """compare_to_random.play_games' loop (compare_to_random.py:16-35) for one
+    game after random.seed(seed), np.random.seed(seed): seat 0 run_mccfr with
+    the model (cfr_pred(pred_iters, 10)), seat 1 run_mccfr(train_iters), both
+    only with > 1 option; other seats random.choice.  `model` maps a game to
+    float32 winning probabilities.  Returns (game, steps, decisions)."""
+    g = O.new_game(seed, True)
+    npr = np.random.RandomState(seed)
+    g.nprng = npr
+    steps, decisions = 0, []
+    while True:
+        pid = g.gs.pid
+        if pid == 0 and len(g.get_options()) > 1:
+            chosen, _ = run_mccfr(g, npr, pred_iters, model=model)
+            decisions.append([0, steps, chosen.canon()])
+            w = g.carry_out(chosen)
+        elif pid == 1 and len(g.get_options()) > 1:
+            chosen, _ = run_mccfr(g, npr, train_iters)
+            decisions.append([1, steps, chosen.canon()])
+            w = g.carry_out(chosen)
+        else:
+            opts = g.get_options()
+            w = g.carry_out(opts[g.rng._randbelow(len(opts))])
+        steps += 1
+        if w is not None:
+            return g, steps, decisions

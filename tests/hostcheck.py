@@ -220,3 +220,28 @@ def split_targets(t):
     for k, (lane, node, pid, nch, c0) in enumerate(t["meta"]):
         per[lane].append((t["feat"][k], t["opt_feat"][c0:c0 + nch], t["value"][k], t["dist"][c0:c0 + nch]))
     return per
+
+
+def compare_game(seed, fma, pred_iters, train_iters, node_cap=2048):
+    """compare_to_random's loop for one game on the host build of the engine:
+    cith_advance_policy between decisions, cith_cfr_pred_step (seat 0, `fma`
+    leaf evaluator) and cith_cfr_decide (seat 1).  Returns (hb, random steps,
+    decisions [(seat, option descriptor, game before carry_out)])."""
+    hb = HostBatch([seed], True)
+    cf = HostCfr(hb, node_cap=node_cap, edge_cap=8 * node_cap)
+    status = np.zeros(1, np.int32)
+    steps = np.zeros(1, np.int32)
+    decisions = []
+    while True:
+        lib().cith_advance_policy(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(hb.seer), C.c_int(1), C.c_int(3),
+                                  C.c_int(-1), _p(status), _p(steps))
+        seat = int(status[0])
+        if seat < 0:
+            return hb, int(steps[0]), decisions
+        if seat == 0:
+            chosen, stats, _ = cfr_pred(cf, pred_iters, 10, fma)
+        else:
+            chosen, stats = cf.decide(train_iters)
+        assert stats[0][4] == 0, stats
+        decisions.append((seat, chosen[0].copy(), hb.game(0)))
+        hb.carry_out(chosen)

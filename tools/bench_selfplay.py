@@ -1,0 +1,101 @@
+"""Measurement of BASELINE.json configs 3-5 (the MCCFR workloads), one process
+per GPU (run under torchrun for N > 1; 1 GPU otherwise):
+
+  --config 3  B positions per GPU, one cfr_train(200) decision each (no NN)
+  --config 4  B positions per GPU, one cfr_pred(200, depth 10) decision each
+              with ValueOnlyNN(418,512) (torch.manual_seed(0) weights,
+              broadcast from rank 0), leaf rows batched into the MFMA kernel
+  --config 5  B simulate_game trees per GPU: create_a_random_game(100) ->
+              cfr_train(M) -> get_all_targets, targets pooled over ranks with
+              the RCCL all-gather
+
+Timed region: barrier + synchronize on both sides, max over ranks; inputs
+(positions) are built before it except for config 5, whose position
+generation is part of simulate_game.  Prints one JSON line (rank 0) with
+decisions/s (or trees/s), carry_out transitions/s inside the searches and
+the per-kernel HIP-event times.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from citadels_self_play_amd import selfplay  # noqa: E402
+from citadels_self_play_amd.engine import GameBatch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=3, choices=(3, 4, 5))
+    ap.add_argument("--batch", type=int, default=None, help="per GPU")
+    ap.add_argument("--iters", type=int, default=None)
+    ap.add_argument("--node-cap", type=int, default=None)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=30_000_000)
+    a = ap.parse_args()
+    rank, world, dev = selfplay.init_distributed()
+    B = a.batch or {3: 1024, 4: 4096 // max(1, world) if world > 1 else 4096, 5: 256}[a.config]
+    iters = a.iters or {3: 200, 4: 200, 5: 20000}[a.config]
+    net = None
+    if a.config == 4:
+        from citadels_self_play_amd import models
+        torch.manual_seed(0)
+        m = selfplay.broadcast_model(models.ValueOnlyNN(418, 512).to(dev).eval())
+        net = models.ValueNet(m, dev)
+    out = []
+    for rep in range(a.reps):
+        seeds = selfplay.shard(B * world, base_seed=a.seed + rep * B * world)
+        b = None
+        if a.config in (3, 4):
+            b = GameBatch(seeds, preset=True, device=dev)
+            b.advance_random(0, 300)
+            b.seed_numpy()
+            term = b.terminal()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        rounds, n_targets = 0, 0
+        if a.config == 3:
+            chosen, stats = b.cfr_decide(iters, node_cap=a.node_cap or 1024)
+        elif a.config == 4:
+            chosen, stats, rounds = b.cfr_pred(iters, net, max_depth=10, node_cap=a.node_cap or 2048)
+        else:
+            b, stats, t = selfplay.simulate_games(seeds, iters, node_cap=a.node_cap)
+            f, v = selfplay.all_gather_targets(t["feat"], t["value"])
+            n_targets = int(f.shape[0])
+            term = b.terminal()            # k = 1 picks the final (terminal) game: ValueError in the reference
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        st = stats.to(dev).to(torch.float64)
+        tot = torch.tensor([el, float(b.B), float(st[:, 3].sum()), float(((st[:, 4] != 0) & ~term).sum()),
+                            float(term.sum()), float(st[:, 1].sum()), float(st[:, 1].max())], dtype=torch.float64,
+                           device=dev)
+        if world > 1:
+            tmax = tot.clone()
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tot)
+            tot[0], tot[6] = tmax[0], tmax[6]
+        el, units, carry, errs, terms, nodes, nodes_max = [float(x) for x in tot]
+        out.append({"config": a.config, "n_gpus": world, "per_gpu": B, "iters": iters, "seconds": el,
+                    ("trees_per_s" if a.config == 5 else "decisions_per_s"): units / el,
+                    "carry_out_per_s": carry / el, "nodes_mean": nodes / units, "nodes_max": int(nodes_max), "rounds": rounds,
+                    "pooled_targets": n_targets, "error_lanes_nonterminal": int(errs),
+                    "terminal_positions": int(terms)})
+    if rank == 0:
+        best = max(out, key=lambda r: r["carry_out_per_s"])
+        print(json.dumps({"best": best, "reps": out}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -3,7 +3,7 @@
 // One tree per workgroup on the device.  The tree lives in HBM as a node
 // pool: CfrNode headers, CfrEdge records (option + child + regret/strategy
 // rows) and one packed game row per node (the reference's `deepcopy(game)`
-// becomes a 1456-byte row copy done by the whole 64-lane team).  Every lane
+// becomes a 1552-byte row copy done by the whole 64-lane team).  Every lane
 // of the team runs the same scalar search code on the same data (uniform
 // control flow, identical writes), so row copies and other data-parallel
 // pieces can be split across lanes without divergence.

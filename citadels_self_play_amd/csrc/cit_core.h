@@ -28,7 +28,7 @@
 #define CIT_NP 6
 #define CIT_HAND_CAP 32
 #define CIT_BUILD_CAP 16
-#define CIT_JD_CAP 24
+#define CIT_JD_CAP 40
 #define CIT_MUSEUM_CAP 16
 #define CIT_DECK_CAP 128          // ring buffer, power of two
 #define CIT_DISCARD_CAP 80
@@ -107,7 +107,7 @@ struct CitOpt {
 };
 
 // ------------------------------------------------------------- packed game
-struct CitPlayer {                 // 112 B
+struct CitPlayer {                 // 128 B
   uint8_t hand[CIT_HAND_CAP];
   uint8_t build[CIT_BUILD_CAP];
   uint8_t jd[CIT_JD_CAP];          // just_drawn_cards
@@ -174,7 +174,7 @@ struct CitGame {
 enum { RP_DEAD = 1, RP_WARRANT_SHIFT = 1, RP_POSSESSED = 8, RP_ROBBED = 16, RP_BLACKMAIL_SHIFT = 5 };
 enum { WB_NONE = 0, WB_REAL = 1, WB_FAKE = 2 };
 
-#define CIT_GAME_BYTES 1456
+#define CIT_GAME_BYTES 1552
 static_assert(sizeof(CitGame) <= CIT_GAME_BYTES, "CitGame grew past its row size");
 static_assert(CIT_GAME_BYTES % 16 == 0, "row must be 16-byte aligned");
 

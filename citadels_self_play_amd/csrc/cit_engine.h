@@ -461,14 +461,12 @@ struct ListSink {
     return false;
   }
   template <class F> CIT_HD bool block(int cnt, F&& f) {
-    for (int i = 0; i < cnt; i++) {
-      if (n < cap) buf[n] = f(i);
-      n++;
-    }
+    int m = cap - n < cnt ? cap - n : cnt;      // materialise up to cap, count the rest
+    for (int i = 0; i < m; i++) buf[n + i] = f(i);
+    n += cnt;
     return false;
   }
 };
-
 #define EMIT(...)                                  \
   do {                                             \
     if (s.emit(__VA_ARGS__)) return true;          \

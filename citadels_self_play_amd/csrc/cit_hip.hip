@@ -1,11 +1,13 @@
 // HIP kernels + C ABI (include/citadels.h) of the MI355X Citadels engine.
 //
-// Execution model: one lane = one game.  A workgroup of G lanes stages its G
-// packed rows (CIT_GAME_BYTES each) from HBM into LDS at an odd-dword stride
-// (same-field accesses of different lanes hit different banks), runs the
-// engine on its lane's row in LDS, and writes the rows back.  The CPython
-// MT19937 streams stay in HBM, structure-of-arrays ([624][B]), so the lanes of
-// a wave twisting together read and write consecutive words.
+// Execution model: one game per 64-lane workgroup with wave-uniform code
+// (uniform_game below): the lanes stage the game's packed row (CIT_GAME_BYTES)
+// and, for multi-step kernels, its 624 CPython-MT19937 words from HBM into
+// LDS; lane 0 runs the engine with every address derived from blockIdx.x, so
+// the game's scalars live in SGPRs and its branches are scalar; the lanes
+// write back.  MT19937 streams are stored structure-of-arrays ([624][B]) in
+// HBM.  k_rollout (games_per_block > 0) keeps the one-game-per-lane layout for
+// sweeps.
 #include <hip/hip_runtime.h>
 
 #include "../../include/citadels.h"
@@ -39,6 +41,42 @@ __device__ __forceinline__ CitMT lane_mt(uint32_t* mt, const uint32_t* idx, int 
   return r;
 }
 
+// One game per 64-lane workgroup with wave-uniform code: the game index is
+// blockIdx.x (never threadIdx.x), so the compiler keeps the game's scalars in
+// SGPRs and branches with s_cbranch instead of exec masks (measured: +27 %
+// transitions/s at B = 4096 over one game per lane, and no scratch spills).
+// The 64 lanes stage the row (and, for multi-step kernels, the 624 MT19937
+// words) into LDS; lane 0 runs `body(game, stream, l)`; the lanes write back.
+template <bool MT_LDS, bool STAGE_ROW, class F>
+__device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, F&& body) {
+  __shared__ __attribute__((aligned(16))) uint32_t row[ROW_W];
+  __shared__ uint32_t mts[MT_LDS ? CIT_MT_N : 1];
+  const long l = blockIdx.x;
+  if (STAGE_ROW)
+    for (int i = threadIdx.x; i < ROW_W; i += blockDim.x) row[i] = games[l * ROW_W + i];
+  if (MT_LDS)
+    for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) mts[i] = mt[(long)i * B + l];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    CitGame& g = *reinterpret_cast<CitGame*>(row);
+    CitMT r;
+    if (MT_LDS) {
+      r.mt = mts;
+      r.stride = 1;
+    } else {
+      r.mt = mt + l;
+      r.stride = B;
+    }
+    r.pos = idx[l];
+    body(g, r, l);
+    idx[l] = r.pos;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ROW_W; i += blockDim.x) games[l * ROW_W + i] = row[i];
+  if (MT_LDS)
+    for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) mt[(long)i * B + l] = mts[i];
+}
+
 __global__ void k_mt_seed(uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int numpy_style) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= B) return;
@@ -64,61 +102,30 @@ __global__ void k_randbelow(uint32_t* mt, uint32_t* idx, int B, uint32_t bound, 
   idx[l] = r.pos;
 }
 
-__global__ void k_init(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int preset) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  long g0 = (long)blockIdx.x * blockDim.x;
-  int nrows = (int)min((long)blockDim.x, (long)B - g0);
-  long l = g0 + threadIdx.x;
-  if (threadIdx.x < nrows) {
-    CitMT r = lane_mt(mt, idx, B, l);
+__global__ __launch_bounds__(64) void k_init(uint32_t* games, uint32_t* mt, uint32_t* idx, int B,
+                                            const uint64_t* seeds, int preset) {
+  uniform_game<true, false>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     if (seeds) mt_seed_cpython(r, seeds[l]);          // NULL: continue the lane's stream
-    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
     cit_init_game(g, r, preset != 0);
-    idx[l] = r.pos;
-  }
-  __syncthreads();
-  stage_out(lds, games, g0, nrows);
+  });
 }
 
-__global__ void k_get_options(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, CitOpt* opts,
-                              int max_opts, int32_t* n_opts) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  long g0 = (long)blockIdx.x * blockDim.x;
-  int nrows = (int)min((long)blockDim.x, (long)B - g0);
-  stage_in(lds, games, g0, nrows);
-  __syncthreads();
-  if (threadIdx.x < nrows) {
-    long l = g0 + threadIdx.x;
-    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
-    CitMT r = lane_mt(mt, idx, B, l);
+__global__ __launch_bounds__(64) void k_get_options(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer,
+                                                   int B, CitOpt* opts, int max_opts, int32_t* n_opts) {
+  uniform_game<false, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     uint64_t* sc = seer + l * CIT_SEER_MAX;
     cit_prepare_options(g, r, sc);
     ListSink s(opts + l * max_opts, max_opts);
     cit_enum_options(g, s, sc);
     g.err |= s.err;
     n_opts[l] = s.n;
-    idx[l] = r.pos;
-  }
-  __syncthreads();
-  stage_out(lds, games, g0, nrows);
+  });
 }
 
-__global__ void k_carry_out(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, const CitOpt* chosen,
-                            int32_t* winner) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  long g0 = (long)blockIdx.x * blockDim.x;
-  int nrows = (int)min((long)blockDim.x, (long)B - g0);
-  stage_in(lds, games, g0, nrows);
-  __syncthreads();
-  if (threadIdx.x < nrows) {
-    long l = g0 + threadIdx.x;
-    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
-    CitMT r = lane_mt(mt, idx, B, l);
-    winner[l] = cit_carry_out(g, chosen[l], r);
-    idx[l] = r.pos;
-  }
-  __syncthreads();
-  stage_out(lds, games, g0, nrows);
+__global__ __launch_bounds__(64) void k_carry_out(uint32_t* games, uint32_t* mt, uint32_t* idx, int B,
+                                                 const CitOpt* chosen, int32_t* winner) {
+  uniform_game<false, true>(games, mt, idx, B,
+                            [&](CitGame& g, CitMT& r, long l) { winner[l] = cit_carry_out(g, chosen[l], r); });
 }
 
 __global__ void k_random_choice(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, const CitOpt* opts,
@@ -143,8 +150,10 @@ __global__ void k_random_choice(uint32_t* games, uint32_t* mt, uint32_t* idx, in
   chosen[l] = opts[l * max_opts + k];
 }
 
-// The hot loop: get_options -> randbelow -> carry_out until a winner, an error
-// or max_steps, entirely on the LDS-resident row.
+// The step loop with G games per wavefront, one per lane (games_per_block =
+// G > 0; kept for sweeps: divergence across a 47-way option switch makes it
+// slower than k_rollout_u at every B measured).  Rows in LDS at an odd-dword
+// stride, MT19937 words in HBM (structure of arrays).
 __global__ void k_rollout(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_steps,
                           int32_t* steps_out, int32_t* winner) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -172,18 +181,28 @@ __global__ void k_rollout(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t
   stage_out(lds, games, g0, nrows);
 }
 
+// The hot loop (default): one game per workgroup (uniform_game), row and
+// MT19937 words in LDS for the whole rollout.
+__global__ __launch_bounds__(64) void k_rollout_u(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
+                                                 int max_steps, int32_t* steps_out, int32_t* winner) {
+  uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
+    uint64_t* sc = seer + l * CIT_SEER_MAX;
+    int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
+    int s = 0;
+    while (!g.terminal && !g.err && s < cap) {
+      cit_random_step(g, r, sc);
+      s++;
+    }
+    if (max_steps < 0 && s >= cap && !g.terminal && !g.err) g.err |= CIT_ERR_STEP_CAP;
+    steps_out[l] += s;
+    winner[l] = g.winner;
+  });
+}
+
 // config-3 position harness: k = random.randint(lo, hi) random steps per lane.
-__global__ void k_advance(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int lo, int hi,
-                          int32_t* steps_out) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  long g0 = (long)blockIdx.x * blockDim.x;
-  int nrows = (int)min((long)blockDim.x, (long)B - g0);
-  stage_in(lds, games, g0, nrows);
-  __syncthreads();
-  if (threadIdx.x < nrows) {
-    long l = g0 + threadIdx.x;
-    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
-    CitMT r = lane_mt(mt, idx, B, l);
+__global__ __launch_bounds__(64) void k_advance(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
+                                               int lo, int hi, int32_t* steps_out) {
+  uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     uint64_t* sc = seer + l * CIT_SEER_MAX;
     int k = lo + (int)mt_randbelow(r, (uint32_t)(hi - lo + 1));
     int s = 0;
@@ -192,67 +211,34 @@ __global__ void k_advance(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t
       s++;
     }
     steps_out[l] = s;
-    idx[l] = r.pos;
-  }
-  __syncthreads();
-  stage_out(lds, games, g0, nrows);
+  });
 }
 
 // compare_to_random's step loop to the next searched decision per lane.
-__global__ void k_advance_policy(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int search_mask,
-                                 int max_steps, int32_t* status, int32_t* steps_out) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  long g0 = (long)blockIdx.x * blockDim.x;
-  int nrows = (int)min((long)blockDim.x, (long)B - g0);
-  stage_in(lds, games, g0, nrows);
-  __syncthreads();
-  if (threadIdx.x < nrows) {
-    long l = g0 + threadIdx.x;
-    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
-    CitMT r = lane_mt(mt, idx, B, l);
+__global__ __launch_bounds__(64) void k_advance_policy(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer,
+                                                      int B, int search_mask, int max_steps, int32_t* status,
+                                                      int32_t* steps_out) {
+  uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     int st = steps_out[l];
     status[l] = cit_advance_policy(g, r, seer + l * CIT_SEER_MAX, search_mask, max_steps, st);
     steps_out[l] = st;
-    idx[l] = r.pos;
-  }
-  __syncthreads();
-  stage_out(lds, games, g0, nrows);
+  });
 }
 
 // create_a_random_game(max_move) per lane (train_from_scratch data generation).
-__global__ void k_random_position(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_move,
-                                  uint32_t* ring, int32_t* steps_out) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  long g0 = (long)blockIdx.x * blockDim.x;
-  int nrows = (int)min((long)blockDim.x, (long)B - g0);
-  if (threadIdx.x < nrows) {
-    long l = g0 + threadIdx.x;
-    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
-    CitMT r = lane_mt(mt, idx, B, l);
+__global__ __launch_bounds__(64) void k_random_position(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer,
+                                                       int B, int max_move, uint32_t* ring, int32_t* steps_out) {
+  uniform_game<true, false>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     steps_out[l] = cit_random_position(g, r, seer + l * CIT_SEER_MAX, ring + l * (long)max_move * ROW_W, max_move);
-    idx[l] = r.pos;
-  }
-  __syncthreads();
-  stage_out(lds, games, g0, nrows);
+  });
 }
 
 // create_a_close_to_finished_game per lane (generate_test_data positions).
-__global__ void k_close_position(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, uint32_t* store,
-                                 int32_t* index) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  long g0 = (long)blockIdx.x * blockDim.x;
-  int nrows = (int)min((long)blockDim.x, (long)B - g0);
-  stage_in(lds, games, g0, nrows);
-  __syncthreads();
-  if (threadIdx.x < nrows) {
-    long l = g0 + threadIdx.x;
-    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
-    CitMT r = lane_mt(mt, idx, B, l);
+__global__ __launch_bounds__(64) void k_close_position(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer,
+                                                      int B, uint32_t* store, int32_t* index) {
+  uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     index[l] = cit_close_position(g, r, seer + l * CIT_SEER_MAX, store + l * (long)CIT_CLOSE_ROWS * ROW_W);
-    idx[l] = r.pos;
-  }
-  __syncthreads();
-  stage_out(lds, games, g0, nrows);
+  });
 }
 
 template <class K>
@@ -264,15 +250,7 @@ size_t lds_bytes(int G) { return (size_t)G * LDS_W * 4; }
 bool g_attrs_done = false;
 int ensure_attrs() {
   if (g_attrs_done) return 0;
-  size_t m = lds_bytes(MAX_G);
-  int e = set_lds(k_init, m);
-  if (!e) e = set_lds(k_get_options, m);
-  if (!e) e = set_lds(k_carry_out, m);
-  if (!e) e = set_lds(k_rollout, m);
-  if (!e) e = set_lds(k_advance, m);
-  if (!e) e = set_lds(k_random_position, m);
-  if (!e) e = set_lds(k_close_position, m);
-  if (!e) e = set_lds(k_advance_policy, m);
+  int e = set_lds(k_rollout, lds_bytes(MAX_G));
   if (!e) g_attrs_done = true;
   return e;
 }
@@ -321,9 +299,7 @@ int cit_randbelow(uint32_t* mt, uint32_t* mt_idx, int B, int bound, int32_t* out
 int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int preset,
              hipStream_t stream) {
   if (B <= 0 || !games || !mt || !mt_idx) return -1;
-  if (int e = ensure_attrs()) return e;
-  const int G = 64;
-  hipLaunchKernelGGL(k_init, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx, B,
+  hipLaunchKernelGGL(k_init, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, B,
                      seeds, preset);
   CHECK_LAUNCH();
 }
@@ -331,9 +307,7 @@ int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t*
 int cit_get_options(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, CitOption* opts,
                     int max_opts, int32_t* n_opts, hipStream_t stream) {
   if (B <= 0 || max_opts < 0 || !games || !mt || !mt_idx || !seer || !n_opts || (max_opts && !opts)) return -1;
-  if (int e = ensure_attrs()) return e;
-  const int G = 64;
-  hipLaunchKernelGGL(k_get_options, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+  hipLaunchKernelGGL(k_get_options, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt,
                      mt_idx, seer, B, (CitOpt*)opts, max_opts, n_opts);
   CHECK_LAUNCH();
 }
@@ -350,9 +324,7 @@ int cit_random_choice(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const 
 int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitOption* chosen, int32_t* winner,
                   hipStream_t stream) {
   if (B <= 0 || !games || !mt || !mt_idx || !chosen || !winner) return -1;
-  if (int e = ensure_attrs()) return e;
-  const int G = 64;
-  hipLaunchKernelGGL(k_carry_out, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+  hipLaunchKernelGGL(k_carry_out, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt,
                      mt_idx, B, (const CitOpt*)chosen, winner);
   CHECK_LAUNCH();
 }
@@ -360,12 +332,16 @@ int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitO
 int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
                        int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream) {
   if (B <= 0 || !games || !mt || !mt_idx || !seer || !steps || !winner) return -1;
-  // 0 = auto: one game per wavefront until the chip has ~4 waves per SIMD
-  // (B = 4096), then more lanes per wave (divergence costs less than idle SIMDs)
-  int G = games_per_block > 0 ? games_per_block : (B >= 8192 ? B / 4096 : 1);
-  if (G > 16 && games_per_block <= 0) G = 16;
-  if (G > MAX_G) return -1;
+  if (games_per_block > MAX_G) return -1;
   if (int e = ensure_attrs()) return e;
+  // 0 = auto: one game per workgroup, wave-uniform code (k_rollout_u)
+  if (games_per_block <= 0) {
+    hipLaunchKernelGGL(k_rollout_u, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, seer, B, max_steps,
+                       steps, winner);
+    CHECK_LAUNCH();
+  }
+  // G lanes = G games per workgroup (one wavefront), per-lane code
+  int G = games_per_block;
   hipLaunchKernelGGL(k_rollout, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx,
                      seer, B, max_steps, steps, winner);
   CHECK_LAUNCH();
@@ -374,9 +350,7 @@ int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
 int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int lo, int hi,
                        int32_t* steps, hipStream_t stream) {
   if (B <= 0 || hi < lo || lo < 0 || !games || !mt || !mt_idx || !seer || !steps) return -1;
-  if (int e = ensure_attrs()) return e;
-  const int G = 1;
-  hipLaunchKernelGGL(k_advance, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx,
+  hipLaunchKernelGGL(k_advance, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx,
                      seer, B, lo, hi, steps);
   CHECK_LAUNCH();
 }
@@ -384,9 +358,7 @@ int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
 int cit_random_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_move,
                         uint32_t* ring, int32_t* steps, hipStream_t stream) {
   if (B <= 0 || max_move <= 0 || !games || !mt || !mt_idx || !seer || !ring || !steps) return -1;
-  if (int e = ensure_attrs()) return e;
-  const int G = 16;
-  hipLaunchKernelGGL(k_random_position, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+  hipLaunchKernelGGL(k_random_position, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt,
                      mt_idx, seer, B, max_move, ring, steps);
   CHECK_LAUNCH();
 }
@@ -396,9 +368,7 @@ int cit_close_rows(void) { return CIT_CLOSE_ROWS; }
 int cit_close_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, uint32_t* store,
                        int32_t* index, hipStream_t stream) {
   if (B <= 0 || !games || !mt || !mt_idx || !seer || !store || !index) return -1;
-  if (int e = ensure_attrs()) return e;
-  const int G = 16;
-  hipLaunchKernelGGL(k_close_position, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+  hipLaunchKernelGGL(k_close_position, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt,
                      mt_idx, seer, B, store, index);
   CHECK_LAUNCH();
 }
@@ -406,9 +376,7 @@ int cit_close_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
 int cit_advance_policy(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int search_mask,
                        int max_steps, int32_t* status, int32_t* steps, hipStream_t stream) {
   if (B <= 0 || !games || !mt || !mt_idx || !seer || !status || !steps) return -1;
-  if (int e = ensure_attrs()) return e;
-  const int G = 1;
-  hipLaunchKernelGGL(k_advance_policy, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt,
+  hipLaunchKernelGGL(k_advance_policy, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt,
                      mt_idx, seer, B, search_mask, max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps, status, steps);
   CHECK_LAUNCH();
 }

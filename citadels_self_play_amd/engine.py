@@ -60,7 +60,7 @@ class GameBatch:
 
     @classmethod
     def from_tensors(cls, games, mt, mt_idx, seer, np_mt=None, np_idx=None):
-        """A batch over existing device state (no init): games [B,1456] u8, mt [624,B],
+        """A batch over existing device state (no init): games [B,1552] u8, mt [624,B],
         mt_idx [B], seer [B,SEER_MAX] and optionally numpy streams np_mt/np_idx."""
         self = cls.__new__(cls)
         self.lib = _lib.load()

@@ -7,10 +7,10 @@ two definitions cannot drift apart silently.
 import ctypes as C
 
 NP = 6
-HAND_CAP, BUILD_CAP, JD_CAP, MUSEUM_CAP = 32, 16, 24, 16
+HAND_CAP, BUILD_CAP, JD_CAP, MUSEUM_CAP = 32, 16, 40, 16
 DECK_CAP, DISCARD_CAP, USED_CAP = 128, 80, 80
 KH_MAX, KH_POOL, SEVEN_CAP = 32, 252, 8
-GAME_BYTES = 1456
+GAME_BYTES = 1552
 MT_N = 624
 SEER_MAX = 5 * HAND_CAP * 3      # CIT_SEER_MAX: packed seer give-back options per lane
 NO_CARD = 255

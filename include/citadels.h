@@ -96,8 +96,9 @@ int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitO
 /* The fused random-policy step loop of compare_to_random.py:37-39 /
  * run_utils.py:37-41 (get_options -> random.choice -> carry_out) for up to
  * max_steps steps per lane (max_steps < 0: until a winner or an error).
- * steps[l] += steps taken; winner[l] as above.  games_per_block (1..64, 0 =
- * default) sets how many lanes share a workgroup's LDS. */
+ * steps[l] += steps taken; winner[l] as above.  games_per_block 0 (default):
+ * one game per workgroup with wave-uniform code, row and MT19937 words in LDS;
+ * 1..64: that many games per wavefront, one per lane. */
 int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
                        int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream);
 

@@ -66,13 +66,19 @@ struct CfrTree {
   uint8_t* tmp;                        // >= CIT_USED_CAP bytes scratch
   uint32_t err;
   uint32_t carry_outs;
-  int lane, team;
 };
 
+// The 64 lanes of a tree's workgroup (one wavefront) run the search in
+// lockstep on shared state (the CfrTree itself lives in LDS); row copies are
+// split across them.
 #if defined(__HIP_DEVICE_COMPILE__)
 #define CFR_SYNC() __syncthreads()
+#define CFR_LANE ((int)threadIdx.x)
+#define CFR_TEAM ((int)blockDim.x)
 #else
 #define CFR_SYNC() ((void)0)
+#define CFR_LANE 0
+#define CFR_TEAM 1
 #endif
 
 // One out-of-line copy of each engine entry point for the search: the
@@ -84,27 +90,55 @@ struct CfrTree {
 #else
 #define CIT_NOINLINE inline
 #endif
-CIT_NOINLINE int eng_carry(CitGame& g, const CitOpt& o, CitMT& r) { return cit_carry_out(g, o, r); }
-CIT_NOINLINE void eng_prepare(CitGame& g, CitMT& r, uint64_t* seer) { cit_prepare_options(g, r, seer); }
+
+// Optional per-function cycle accounting (build with -DCIT_PROF; debugging only).
+#if defined(CIT_PROF) && defined(__HIPCC__)
+__device__ unsigned long long g_cit_prof[32];
+#endif
+#if defined(CIT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+struct CitProf {
+  int id;
+  unsigned long long t0;
+  __device__ explicit CitProf(int i) : id(i), t0(clock64()) {}
+  __device__ ~CitProf() {
+    if (threadIdx.x == 0) {
+      atomicAdd(&g_cit_prof[id], clock64() - t0);
+      atomicAdd(&g_cit_prof[16 + id], 1ull);
+    }
+  }
+};
+#define CIT_PROF_SCOPE(i) CitProf _cit_prof_scope(i)
+#else
+#define CIT_PROF_SCOPE(i) ((void)0)
+#endif
+CIT_NOINLINE int eng_carry(CitGame& g, const CitOpt& o, CitMT& r) {
+  CIT_PROF_SCOPE(0); return cit_carry_out(g, o, r); }
+CIT_NOINLINE void eng_prepare(CitGame& g, CitMT& r, uint64_t* seer) {
+  CIT_PROF_SCOPE(1); cit_prepare_options(g, r, seer); }
 CIT_NOINLINE int eng_count(const CitGame& g, uint32_t& err, const uint64_t* seer) {
+  CIT_PROF_SCOPE(2);
   return cit_count_options(g, err, seer);
 }
-CIT_NOINLINE CitOpt eng_pick(const CitGame& g, int k, const uint64_t* seer) { return cit_pick_option(g, k, seer); }
+CIT_NOINLINE CitOpt eng_pick(const CitGame& g, int k, const uint64_t* seer) {
+  CIT_PROF_SCOPE(3); return cit_pick_option(g, k, seer); }
 CIT_NOINLINE int eng_list(const CitGame& g, CitOpt* buf, int cap, uint32_t& err, const uint64_t* seer) {
+  CIT_PROF_SCOPE(4);
   ListSink s(buf, cap);
   cit_enum_options(g, s, seer);
   err |= s.err;
   return s.n;
 }
 CIT_NOINLINE void eng_sample(CitGame& g, int orig, bool role_sample, CitMT& r, uint8_t* unk) {
+  CIT_PROF_SCOPE(5);
   cit_sample_private(g, orig, role_sample, r, unk);
 }
 
 CIT_HD uint32_t* row_of(const CfrTree& T, int id) { return T.rows + (long)id * (CIT_GAME_BYTES / 4); }
 // deepcopy(game): the team copies one row
 CIT_NOINLINE void copy_row(const CfrTree& T, uint32_t* dst, const uint32_t* src) {
+  CIT_PROF_SCOPE(6);
   CFR_SYNC();
-  for (int i = T.lane; i < CIT_GAME_BYTES / 4; i += T.team) dst[i] = src[i];
+  for (int i = CFR_LANE; i < CIT_GAME_BYTES / 4; i += CFR_TEAM) dst[i] = src[i];
   CFR_SYNC();
 }
 
@@ -256,6 +290,7 @@ CIT_NOINLINE void tree_carry(CfrTree& T, CitGame& g, const CitOpt& o, int& winne
 // CFRNode(game=w, parent, depth): skip_false_choice on w, then a new node
 // whose row is w.  Returns the node id (-1 on error).
 CIT_NOINLINE int cfr_node(CfrTree& T, CitGame& w, int parent, int depth) {
+  CIT_PROF_SCOPE(7);
   uint32_t e = 0;
   eng_prepare(w, T.py, T.seer);
   int n = eng_count(w, e, T.seer);
@@ -302,7 +337,8 @@ CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
 }
 
 // ------------------------------------------------------------ expansion
-CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T, int n) {            // :102-131
+CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T, int n) {
+  CIT_PROF_SCOPE(8);            // :102-131
   int f = alloc_edges(T, CFR_ROLE_CHILDREN);
   if (f < 0) return;
   T.nodes[n].first_edge = f;
@@ -334,7 +370,8 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T, int n) {            // :102-1
   }
 }
 
-CIT_NOINLINE void cfr_expand_own(CfrTree& T, int n) {                   // :133-151
+CIT_NOINLINE void cfr_expand_own(CfrTree& T, int n) {
+  CIT_PROF_SCOPE(9);                   // :133-151
   CitGame& g = *T.w0;
   copy_row(T, reinterpret_cast<uint32_t*>(&g), row_of(T, n));
   eng_prepare(g, T.py, T.seer);
@@ -371,7 +408,8 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T, int n) {                   // :133-
   }
 }
 
-CIT_NOINLINE void cfr_expand_opponent(CfrTree& T, int n) {              // :153-179
+CIT_NOINLINE void cfr_expand_opponent(CfrTree& T, int n) {
+  CIT_PROF_SCOPE(10);              // :153-179
   CfrNode& N = T.nodes[n];
   copy_row(T, reinterpret_cast<uint32_t*>(T.w1), row_of(T, n));
   CitGame& h = *T.w1;
@@ -418,7 +456,8 @@ CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
 }
 
 // ---------------------------------------------------------- strategies
-CIT_NOINLINE void cfr_update_strategy(CfrTree& T, int n) {               // :292-319
+CIT_NOINLINE void cfr_update_strategy(CfrTree& T, int n) {
+  CIT_PROF_SCOPE(11);               // :292-319
   CfrNode& N = T.nodes[n];
   int nch = N.n_children;
   if (nch == 0) return;
@@ -458,6 +497,7 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T, int n) {               // :292
 
 // action_choice(live=False) (:67-91): returns the edge index within the node
 CIT_NOINLINE int cfr_choose(CfrTree& T, int n) {
+  CIT_PROF_SCOPE(12);
   CfrNode& N = T.nodes[n];
   int nch = N.n_children;
   const CfrEdge* E = T.edges + (N.first_edge < 0 ? 0 : N.first_edge);
@@ -482,7 +522,8 @@ CIT_NOINLINE int cfr_choose(CfrTree& T, int n) {
 }
 
 // ------------------------------------------------------------- backup
-CIT_NOINLINE void cfr_update_regrets(CfrTree& T, int n) {                // :231-256
+CIT_NOINLINE void cfr_update_regrets(CfrTree& T, int n) {
+  CIT_PROF_SCOPE(13);                // :231-256
   CfrNode& N = T.nodes[n];
   CfrEdge* E = T.edges + N.first_edge;
   int nch = N.n_children;
@@ -504,7 +545,8 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T, int n) {                // :231
   }
 }
 
-CIT_NOINLINE void cfr_backprop(CfrTree& T, int n, const double* reward, bool model) {   // :276-290
+CIT_NOINLINE void cfr_backprop(CfrTree& T, int n, const double* reward, bool model) {
+  CIT_PROF_SCOPE(14);   // :276-290
   while (n >= 0) {
     CfrNode& N = T.nodes[n];
     double s0 = 0.0;
@@ -550,6 +592,7 @@ CIT_HD int cfr_train(CfrTree& T, int iters) {
 
 // action_choice(live=True) at the root (:67-91; game.py:312-317 for a role pick).
 CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T, int root) {
+  CIT_PROF_SCOPE(15);
   CfrNode& N = T.nodes[root];
   if (!(N.flags & NF_ROLE_PICK)) {
     int a = cfr_choose(T, root);
@@ -607,7 +650,7 @@ CIT_NOINLINE void cfr_write_feat(CfrTree& T, int n, float* feat) {
   const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
   int pid = (T.nodes[n].flags & NF_ROLE_PICK) ? 5 : -1;
   CFR_SYNC();
-  if (T.lane == 0) cit_encode_game(g, feat, pid);
+  if (CFR_LANE == 0) cit_encode_game(g, feat, pid);
   CFR_SYNC();
 }
 

@@ -17,6 +17,23 @@ __device__ __forceinline__ CitMT lane_mt(uint32_t* mt, const uint32_t* idx, int 
   return r;
 }
 
+// The tree's two streams (CPython `random`, numpy `np.random`) live in LDS for
+// the whole launch: every draw of the search is an LDS access instead of a
+// strided HBM one.
+__device__ __forceinline__ CitMT mt_stage_in(uint32_t* dst, const uint32_t* mt, const uint32_t* idx, int B, long l) {
+  for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) dst[i] = mt[(long)i * B + l];
+  __syncthreads();
+  CitMT r;
+  r.mt = dst;
+  r.stride = 1;
+  r.pos = idx[l];
+  return r;
+}
+__device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, int B, long l) {
+  __syncthreads();
+  for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) mt[(long)i * B + l] = src[i];
+}
+
 // One MCCFR decision per workgroup: a 64-lane team runs the search on its
 // tree (node pool in HBM, working rows in LDS).
 __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
@@ -30,7 +47,7 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   if (l >= B) return;
   long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
   uint8_t* base = pool + per * l;
-  CfrTree T;
+  __shared__ CfrTree T;     // shared: the wavefront's lanes update it in lockstep
   T.nodes = reinterpret_cast<CfrNode*>(base);
   T.edges = reinterpret_cast<CfrEdge*>(base + (long)node_cap * sizeof(CfrNode));
   T.rows = reinterpret_cast<uint32_t*>(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
@@ -38,8 +55,9 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   T.edge_cap = edge_cap;
   T.n_nodes = T.n_edges = 0;
   T.training = false;
-  T.py = lane_mt(mt, idx, B, l);
-  T.np = lane_mt(npmt, npidx, B, l);
+  __shared__ uint32_t pys[CIT_MT_N], nps[CIT_MT_N];
+  T.py = mt_stage_in(pys, mt, idx, B, l);
+  T.np = mt_stage_in(nps, npmt, npidx, B, l);
   T.seer = seer + l * CIT_SEER_MAX;
   T.optbuf = optbuf + l * CFR_OPT_CAP;
   T.w0 = reinterpret_cast<CitGame*>(w0s);
@@ -47,14 +65,14 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   T.tmp = tmps;
   T.err = 0;
   T.carry_outs = 0;
-  T.lane = threadIdx.x;
-  T.team = blockDim.x;
   copy_row(T, w0s, games + l * ROW_W);
   T.orig = T.w0->gs_pid;
   int root = cfr_train(T, iters);
   CitOpt c = mk(O_NUM_NAMES, 0);
   if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
   if (root >= 0) copy_row(T, games + l * ROW_W, row_of(T, root));
+  mt_stage_out(pys, mt, B, l);
+  mt_stage_out(nps, npmt, B, l);
   if (threadIdx.x == 0) {
     chosen[l] = c;
     idx[l] = T.py.pos;
@@ -79,26 +97,26 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   __shared__ __attribute__((aligned(16))) uint8_t tmps[128];
   long l = blockIdx.x;
   if (l >= B) return;
-  CfrState S = state[l];
+  __shared__ CfrState S;
+  S = state[l];             // every lane stores the same value
   if (S.phase == CP_DONE) return;
   long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
   uint8_t* base = pool + per * l;
-  CfrTree T;
+  __shared__ CfrTree T;     // shared: the wavefront's lanes update it in lockstep
   T.nodes = reinterpret_cast<CfrNode*>(base);
   T.edges = reinterpret_cast<CfrEdge*>(base + (long)node_cap * sizeof(CfrNode));
   T.rows = reinterpret_cast<uint32_t*>(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
   T.node_cap = node_cap;
   T.edge_cap = edge_cap;
   T.training = false;
-  T.py = lane_mt(mt, idx, B, l);
-  T.np = lane_mt(npmt, npidx, B, l);
+  __shared__ uint32_t pys[CIT_MT_N], nps[CIT_MT_N];
+  T.py = mt_stage_in(pys, mt, idx, B, l);
+  T.np = mt_stage_in(nps, npmt, npidx, B, l);
   T.seer = seer + l * CIT_SEER_MAX;
   T.optbuf = optbuf + l * CFR_OPT_CAP;
   T.w0 = reinterpret_cast<CitGame*>(w0s);
   T.w1 = reinterpret_cast<CitGame*>(w1s);
   T.tmp = tmps;
-  T.lane = threadIdx.x;
-  T.team = blockDim.x;
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;
@@ -112,6 +130,8 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   int r = cfr_pred_run(T, S, iters, max_depth, probs + 6 * l, feat + (long)CIT_FEAT * l, c);
   cfr_state_save(T, S);
   if (!r && S.root >= 0) copy_row(T, games + l * ROW_W, row_of(T, S.root));
+  mt_stage_out(pys, mt, B, l);
+  mt_stage_out(nps, npmt, B, l);
   if (threadIdx.x == 0) {
     state[l] = S;
     if (!r) chosen[l] = c;
@@ -201,5 +221,14 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
                      (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting);
   CHECK_LAUNCH();
 }
+
+#if defined(CIT_PROF)
+int cit_prof_read(unsigned long long* out) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cit_prof), sizeof(unsigned long long) * 32);
+  unsigned long long z[32] = {0};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_cit_prof), z, sizeof(z));
+  return (int)e;
+}
+#endif
 
 }  // extern "C"

@@ -1455,8 +1455,8 @@ CIT_HD void kr_strip(const CitGame& g, uint16_t* kr, int role) {
 }
 
 // Game.sample_private_information(players[orig], role_sample) (game.py:215-339):
-// resample everything `orig` cannot see.  `unk` is >= CIT_USED_CAP bytes of
-// scratch (LDS on the device).
+// resample everything `orig` cannot see.  `unk` is >= CIT_USED_CAP + 40 bytes
+// of scratch (LDS on the device).
 CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rng, uint8_t* unk) {
   CitPlayer& PC = g.pl[orig];
   // hk.used with probability (confidence-1)*0.2 (:217-222)
@@ -1467,23 +1467,34 @@ CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rn
     bool used = (double)(kh_conf(k) - 1) * 0.2 > r;
     k.conf_flags = (uint8_t)((k.conf_flags & ~0x20) | (used ? 0x20 : 0));
   }
-  // get_unknown_cards (:183-213)
-  uint8_t nu = g.n_used_cards;
-  for (int i = 0; i < nu; i++) unk[i] = g.used_cards[i];
+  // get_unknown_cards (:183-213): used_cards minus every visible / known card,
+  // each removal taking the first remaining card of its type.  Removals of one
+  // type never move another type's first occurrence, so the sequence of
+  // get_a_card_like_it calls equals dropping the first k_t cards of each type t
+  // (k_t = removals of type t) in one ordered pass.
+  uint8_t* kt = unk + CIT_USED_CAP;
+  for (int t = 0; t < 40; t++) kt[t] = 0;
   for (int p = 0; p < CIT_NP; p++)
-    for (int i = 0; i < g.pl[p].n_build; i++) take_like(unk, nu, g.pl[p].build[i]);
+    for (int i = 0; i < g.pl[p].n_build; i++) kt[card_type(g.pl[p].build[i])]++;
   for (int p = 0; p < CIT_NP; p++)
-    for (int i = 0; i < g.pl[p].n_museum; i++) take_like(unk, nu, g.pl[p].museum[i]);
-  for (int i = 0; i < PC.n_hand; i++) take_like(unk, nu, PC.hand[i]);
+    for (int i = 0; i < g.pl[p].n_museum; i++) kt[card_type(g.pl[p].museum[i])]++;
+  for (int i = 0; i < PC.n_hand; i++) kt[card_type(PC.hand[i])]++;
   {
     int off = 0;
     for (int e = 0; e < g.n_kh; e++) {
       const CitKH& k = g.kh[e];
       if (k.owner == orig && (k.conf_flags & 0x20))
-        for (int i = 0; i < k.len; i++) take_like(unk, nu, g.kh_pool[off + i]);
+        for (int i = 0; i < k.len; i++) kt[card_type(g.kh_pool[off + i])]++;
       off += k.len;
     }
   }
+  uint8_t nu = 0;
+  for (int i = 0; i < g.n_used_cards; i++) {
+    int c = g.used_cards[i], t = card_type(c);
+    if (kt[t]) kt[t]--;
+    else unk[nu++] = (uint8_t)c;
+  }
+  int head = 0;                                  // unk[head..nu): the undealt unknown cards
   // sample_deck (:245-262): lighthouse knowledge first, then shuffled unknowns
   {
     int n = g.n_deck;
@@ -1501,7 +1512,7 @@ CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rn
       n -= kk;
     }
     shuffle_arr(rng, unk, nu);
-    for (int i = 0; i < n; i++) deck_put(g, pop_front(unk, nu));
+    for (int i = 0; i < n; i++) deck_put(g, head < nu ? unk[head++] : CIT_NO_CARD);
   }
   // sample_warrants_and_blackmails (:321-336)
   for (int which = 0; which < 2; which++) {
@@ -1543,7 +1554,7 @@ CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rn
         for (int i = 0; i < kk; i++) put_card(g, HAND(Q), g.kh_pool[ho + i]);
         n -= kk;
       }
-      for (int i = 0; i < n; i++) put_card(g, HAND(Q), pop_front(unk, nu));
+      for (int i = 0; i < n; i++) put_card(g, HAND(Q), head < nu ? unk[head++] : CIT_NO_CARD);
     }
     // sample_roles_for_opponent (:283-295)
     if (role_sample && p != orig && p != g.gs_pid && g.gs_state != 0) {

@@ -172,8 +172,6 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
     T.tmp = tmp;
     T.err = 0;
     T.carry_outs = 0;
-    T.lane = 0;
-    T.team = 1;
     memcpy(w0, &g[l], CIT_GAME_BYTES);
     int root = cfr_train(T, iters);
     CitOpt c = mk(O_NUM_NAMES, 0);
@@ -227,8 +225,6 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
     T.w0 = w0;
     T.w1 = w1;
     T.tmp = tmp;
-    T.lane = 0;
-    T.team = 1;
     if (S.phase == CP_INIT) {
       T.n_nodes = T.n_edges = 0;
       T.err = 0;

@@ -467,6 +467,27 @@ struct ListSink {
     return false;
   }
 };
+// The step loop's sink: lists the first `cap` options into `buf` (LDS in the
+// rollout kernel) while counting all of them.
+struct BufSink {
+  CitOpt* buf;
+  int cap;
+  int n = 0;
+  uint32_t err = 0;
+  CIT_HD BufSink(CitOpt* b, int c) : buf(b), cap(c) {}
+  CIT_HD bool emit(const CitOpt& o) {
+    if (n < cap) buf[n] = o;
+    n++;
+    return false;
+  }
+  template <class F> CIT_HD bool block(int cnt, F&& f) {
+    int m = cap - n < cnt ? cap - n : cnt;
+    for (int i = 0; i < m; i++) buf[n + i] = f(i);
+    n += cnt;
+    return false;
+  }
+};
+
 #define EMIT(...)                                  \
   do {                                             \
     if (s.emit(__VA_ARGS__)) return true;          \
@@ -1668,6 +1689,22 @@ CIT_HD void cit_encode_option(const CitOpt& o, const CitGame& g, F* out) {
     default:
       break;
   }
+}
+
+// cit_random_step with one enumeration pass in the common case: the options
+// are listed into `buf` while counted and the draw indexes the buffer; only a
+// list longer than `cap` is enumerated again up to the drawn index.
+CIT_HD int cit_random_step_buf(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* buf, int cap) {
+  cit_prepare_options(g, rng, seer);
+  BufSink s(buf, cap);
+  cit_enum_options(g, s, seer);
+  if (s.err) { g.err |= s.err; return 1; }
+  int n = s.n;
+  if (n == 0) { g.err |= CIT_ERR_EMPTY; return 1; }
+  int k = (int)mt_randbelow(rng, (uint32_t)n);
+  CitOpt o = k < cap ? buf[k] : cit_pick_option(g, k, seer);
+  int w = cit_carry_out(g, o, rng);
+  return (w >= 0 || g.err || g.terminal) ? 1 : 0;
 }
 
 // One random-policy step (compare_to_random.py:37-39): get_options ->

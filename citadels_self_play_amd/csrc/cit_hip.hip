@@ -18,6 +18,9 @@ static_assert(sizeof(CitOpt) == sizeof(CitOption), "descriptor layouts differ");
 #define ROW_W (CIT_GAME_BYTES / 4)
 #define LDS_W (ROW_W + 1)
 #define MAX_G 64
+#ifndef ROLLOUT_BUF
+#define ROLLOUT_BUF 32
+#endif
 
 namespace {
 
@@ -185,12 +188,14 @@ __global__ void k_rollout(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t
 // MT19937 words in LDS for the whole rollout.
 __global__ __launch_bounds__(64) void k_rollout_u(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
                                                  int max_steps, int32_t* steps_out, int32_t* winner) {
+  __shared__ __attribute__((aligned(16))) CitOpt buf[ROLLOUT_BUF ? ROLLOUT_BUF : 1];
   uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     uint64_t* sc = seer + l * CIT_SEER_MAX;
     int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
     int s = 0;
     while (!g.terminal && !g.err && s < cap) {
-      cit_random_step(g, r, sc);
+      if (ROLLOUT_BUF) cit_random_step_buf(g, r, sc, buf, ROLLOUT_BUF);
+      else cit_random_step(g, r, sc);
       s++;
     }
     if (max_steps < 0 && s >= cap && !g.terminal && !g.err) g.err |= CIT_ERR_STEP_CAP;

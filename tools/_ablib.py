@@ -1,0 +1,8 @@
+"""A/B a rollout-kernel build: python tools/_ablib.py build/libX.so [B]"""
+import json, os, subprocess, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import citadels_self_play_amd._lib as LL
+LL.LIB_PATH = sys.argv[1]
+sys.argv = ["bench.py", "--no-cpu-baseline", "--steps", "10"] + (["--batch", sys.argv[2]] if len(sys.argv) > 2 else [])
+import bench
+bench.main()

@@ -229,19 +229,52 @@ CIT_HDI void mt_seed_cpython(CitMT& r, uint64_t seed) {
   r.pos = CIT_MT_N;
 }
 
-CIT_HDI void mt_twist(const CitMT& r) {
-  uint32_t cur = mt_word(r, 0);
-  for (int i = 0; i < CIT_MT_N; i++) {
-    // the last word pairs with the already-rewritten mt[0], as in genrand's tail step
-    uint32_t nxt = (i + 1 < CIT_MT_N) ? mt_word(r, i + 1) : mt_word(r, 0);
-    uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
-    int m = i + 397;
-    uint32_t far = m < CIT_MT_N ? mt_word(r, m) : mt_word(r, m - CIT_MT_N);
-    uint32_t v = far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    mt_set(r, i, v);
-    cur = nxt;
+#if defined(CIT_PROF_ROLLOUT) && defined(__HIPCC__)
+__device__ unsigned long long g_roll_prof[160];
+#endif
+#if defined(CIT_PROF_ROLLOUT) && defined(__HIP_DEVICE_COMPILE__)
+struct CitTwistProf {
+  unsigned long long t0 = clock64();
+  __device__ ~CitTwistProf() {
+    atomicAdd(&g_roll_prof[6], clock64() - t0);
+    atomicAdd(&g_roll_prof[7], 1ull);
+  }
+};
+#define CIT_TWIST_PROF() CitTwistProf _twist_prof
+#else
+#define CIT_TWIST_PROF() ((void)0)
+#endif
+
+// genrand's twist in chunks of 16 words: every load of a chunk is issued
+// before its stores, so one memory round trip covers 16 words.  Within a
+// chunk [c, c+16) the loads are mt[c..c+16] (old, or the rewritten mt[0] for
+// the last word) and mt[i+397 mod 624] (old for i < 227, rewritten by an
+// earlier chunk for i >= 227, since 227 > 16): the serial recurrence exactly.
+#define CIT_TWIST_CHUNK 16
+#ifdef CIT_TWIST_NOINLINE
+#define CIT_TWIST_ATTR __attribute__((noinline))
+#else
+#define CIT_TWIST_ATTR
+#endif
+CIT_HDI CIT_TWIST_ATTR void mt_twist(const CitMT& r) {
+  CIT_TWIST_PROF();
+  for (int c = 0; c < CIT_MT_N; c += CIT_TWIST_CHUNK) {
+    uint32_t w[CIT_TWIST_CHUNK + 1], f[CIT_TWIST_CHUNK];
+#pragma unroll
+    for (int j = 0; j <= CIT_TWIST_CHUNK; j++) w[j] = mt_word(r, c + j < CIT_MT_N ? c + j : 0);
+#pragma unroll
+    for (int j = 0; j < CIT_TWIST_CHUNK; j++) {
+      int m = c + j + 397;
+      f[j] = mt_word(r, m < CIT_MT_N ? m : m - CIT_MT_N);
+    }
+#pragma unroll
+    for (int j = 0; j < CIT_TWIST_CHUNK; j++) {
+      uint32_t y = (w[j] & 0x80000000u) | (w[j + 1] & 0x7fffffffu);
+      mt_set(r, c + j, f[j] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
+    }
   }
 }
+static_assert(CIT_MT_N % CIT_TWIST_CHUNK == 0 && CIT_TWIST_CHUNK < 227, "twist chunking");
 
 CIT_HD uint32_t mt_next(CitMT& r) {
   uint32_t i = r.pos;

@@ -184,6 +184,36 @@ __global__ void k_rollout(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t
   stage_out(lds, games, g0, nrows);
 }
 
+#ifdef CIT_PROF_ROLLOUT
+// Phase cycle accounting of the rollout step (profiling builds only:
+// tools/prof_rollout.py).  [0..4] prepare / enumerate / randbelow / pick /
+// carry_out cycles, [5] steps, [16+s] enumerate+carry cycles in state s,
+// [32+s] steps in state s, [64+o] carry_out cycles of option name o, [112+o] their count.
+__device__ int prof_step(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* buf, int cap, unsigned long long* acc) {
+  int st = g.gs_state;
+  unsigned long long t0 = wall_clock64(), t0c = clock64();
+  cit_prepare_options(g, rng, seer);
+  unsigned long long t1 = clock64();
+  BufSink s(buf, cap);
+  cit_enum_options(g, s, seer);
+  unsigned long long t2 = clock64();
+  if (s.err) { g.err |= s.err; return 1; }
+  int n = s.n;
+  if (n == 0) { g.err |= CIT_ERR_EMPTY; return 1; }
+  int k = (int)mt_randbelow(rng, (uint32_t)n);
+  unsigned long long t3 = clock64();
+  CitOpt o = k < cap ? buf[k] : cit_pick_option(g, k, seer);
+  unsigned long long t4 = clock64();
+  int w = cit_carry_out(g, o, rng);
+  unsigned long long t5 = clock64();
+  (void)t0;
+  acc[0] += t1 - t0c; acc[1] += t2 - t1; acc[2] += t3 - t2; acc[3] += t4 - t3; acc[4] += t5 - t4; acc[5] += 1;
+  if (st < 11) { acc[16 + st] += (t2 - t1) + (t5 - t4); acc[32 + st] += 1; }
+  if (o.name < 47) { acc[64 + o.name] += t5 - t4; acc[112 + o.name] += 1; }
+  return (w >= 0 || g.err || g.terminal) ? 1 : 0;
+}
+#endif
+
 // The hot loop (default): one game per workgroup (uniform_game), row and
 // MT19937 words in LDS for the whole rollout.
 __global__ __launch_bounds__(64) void k_rollout_u(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
@@ -193,11 +223,20 @@ __global__ __launch_bounds__(64) void k_rollout_u(uint32_t* games, uint32_t* mt,
     uint64_t* sc = seer + l * CIT_SEER_MAX;
     int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
     int s = 0;
+#ifdef CIT_PROF_ROLLOUT
+    unsigned long long acc[160] = {};
+    while (!g.terminal && !g.err && s < cap) {
+      prof_step(g, r, sc, buf, ROLLOUT_BUF, acc);
+      s++;
+    }
+    for (int i = 0; i < 160; i++) atomicAdd(&g_roll_prof[i], acc[i]);
+#else
     while (!g.terminal && !g.err && s < cap) {
       if (ROLLOUT_BUF) cit_random_step_buf(g, r, sc, buf, ROLLOUT_BUF);
       else cit_random_step(g, r, sc);
       s++;
     }
+#endif
     if (max_steps < 0 && s >= cap && !g.terminal && !g.err) g.err |= CIT_ERR_STEP_CAP;
     steps_out[l] += s;
     winner[l] = g.winner;
@@ -269,6 +308,15 @@ int ensure_attrs() {
   } while (0)
 
 extern "C" {
+
+#ifdef CIT_PROF_ROLLOUT
+int cit_roll_prof_read(unsigned long long* out) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_roll_prof), sizeof(unsigned long long) * 160);
+  unsigned long long z[160] = {};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_roll_prof), z, sizeof(z));
+  return (int)e;
+}
+#endif
 
 int cit_abi_version(void) { return 1; }
 int cit_game_bytes(void) { return CIT_GAME_BYTES; }

@@ -21,6 +21,7 @@ from . import layout as L
 NODE_DT = np.dtype([("parent", "<i4"), ("first_edge", "<i4"), ("n_children", "<i2"), ("edge_cap", "<i2"),
                     ("depth", "<i2"), ("player", "i1"), ("gs_state", "i1"), ("flags", "u1"), ("winner", "i1"),
                     ("pad", "u1", 6), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
+ERR_OVERFLOW = 0x1         # CIT_ERR_OVERFLOW (csrc/cit_core.h)
 EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8", 6), ("S", "<f8", 6),
                     ("CS", "<f8", 6)])
 
@@ -132,11 +133,45 @@ class GameBatch:
         _lib.check(self.lib.cit_mt_seed(_ptr(self.np_mt), _ptr(self.np_idx), self.B, _ptr(seeds), 1, _stream()),
                    "cit_mt_seed")
 
-    def cfr_decide(self, iters, node_cap=1024, edge_cap=None):
+    def _snapshot(self):
+        return tuple(t.clone() for t in (self.games, self.mt, self.mt_idx, self.seer, self.np_mt, self.np_idx,
+                                         self.steps))
+
+    def _retry_overflow(self, snap, stats, chosen, run, max_retries):
+        """Lanes whose search overflowed its node / edge pool (stats err bit
+        CIT_ERR_OVERFLOW) are searched again from their pre-search state with a
+        4x larger pool; results and streams are scattered back, and the
+        sub-batch is kept so cfr_targets can read those lanes' trees."""
+        self._retry = None
+        over = ((stats[:, 4].to(self.device) & ERR_OVERFLOW) != 0).nonzero().flatten()
+        if max_retries <= 0 or over.numel() == 0:
+            return chosen, stats
+        g, mt, idx, seer, npm, npi, steps = snap
+        sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),
+                                     seer[over].contiguous(), npm[:, over].contiguous(), npi[over].contiguous())
+        sub.steps = steps[over].contiguous()
+        c2, s2 = run(sub, 4 * self.node_cap, 4 * self.edge_cap, max_retries - 1)
+        self.scatter(sub, over)
+        chosen = chosen.clone()
+        stats = stats.clone()
+        chosen[over.to(chosen.device)] = c2.to(chosen.device)
+        stats[over.to(stats.device)] = s2.to(stats.device)
+        self._retry = (over, sub)
+        return chosen, stats
+
+    def cfr_decide(self, iters, node_cap=1024, edge_cap=None, max_retries=3):
         """run_mccfr(game, max_iterations=iters) (no model) on every lane; returns
-        (chosen [B,16] uint8 descriptors, stats [B,5] = root, nodes, edges, carry_outs, err)."""
+        (chosen [B,16] uint8 descriptors, stats [B,5] = root, nodes, edges, carry_outs, err).
+        A tree that outgrows its pool is searched again with a 4x pool (up to
+        `max_retries` times), so pool capacity never changes a result."""
         if not hasattr(self, "np_mt"):
             self.seed_numpy()
+        snap = self._snapshot() if max_retries > 0 else None
+        chosen, stats = self._cfr_decide(iters, node_cap, edge_cap)
+        return self._retry_overflow(snap, stats, chosen,
+                                    lambda sub, nc, ec, mr: sub.cfr_decide(iters, nc, ec, mr), max_retries)
+
+    def _cfr_decide(self, iters, node_cap, edge_cap):
         self._pool(node_cap, edge_cap)
         node_cap, edge_cap = self.node_cap, self.edge_cap
         chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
@@ -211,6 +246,21 @@ class GameBatch:
         f32, counts [B,2]."""
         d = self.device
         roots = roots.to(device=d, dtype=torch.int32).contiguous()
+        retry = getattr(self, "_retry", None)
+        if retry is not None:
+            over, sub = retry
+            roots = roots.clone()
+            sub_roots = roots[over].clone()
+            roots[over] = -1
+            main = self._cfr_targets(roots, mode)
+            extra = sub.cfr_targets(sub_roots, mode)
+            self.mt[:, over] = sub.mt
+            self.mt_idx[over] = sub.mt_idx
+            return _merge_targets(main, extra, over)
+        return self._cfr_targets(roots, mode)
+
+    def _cfr_targets(self, roots, mode):
+        d = self.device
         counts = torch.zeros((self.B, 2), dtype=torch.int32, device=d)
         _lib.check(self.lib.cit_cfr_target_count(_ptr(self.pool), self.B, self.node_cap, self.edge_cap, _ptr(roots),
                                                  int(mode), _ptr(counts), _stream()), "cit_cfr_target_count")
@@ -240,13 +290,26 @@ class GameBatch:
             self.optbuf = torch.empty((self.B, self.lib.cit_cfr_opt_cap(), 16), dtype=torch.uint8, device=self.device)
         self.node_cap, self.edge_cap = node_cap, edge_cap
 
-    def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000):
+    def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000, max_retries=3):
         """run_mccfr(game, model, max_iterations=iters) with a model and training=False
         (cfr_pred(iters, max_depth) + live action choice) on every lane.  `net` is a
         models.ValueNet; leaf rows of all suspended trees are evaluated in one MFMA
-        launch per round.  Returns (chosen, stats [B,5], rounds)."""
+        launch per round.  Trees that outgrow their pool are searched again with
+        a 4x pool (as cfr_decide).  Returns (chosen, stats [B,5], rounds)."""
         if not hasattr(self, "np_mt"):
             self.seed_numpy()
+        snap = self._snapshot() if max_retries > 0 else None
+        chosen, stats, rounds = self._cfr_pred(iters, net, max_depth, node_cap, edge_cap, max_rounds)
+        box = [rounds]
+
+        def run(sub, nc, ec, mr):
+            c, st, r = sub.cfr_pred(iters, net, max_depth, nc, ec, max_rounds, mr)
+            box[0] += r
+            return c, st
+        chosen, stats = self._retry_overflow(snap, stats, chosen, run, max_retries)
+        return chosen, stats, box[0]
+
+    def _cfr_pred(self, iters, net, max_depth, node_cap, edge_cap, max_rounds):
         self._pool(node_cap, edge_cap)
         d = self.device
         state = torch.zeros((self.B, self.lib.cit_cfr_state_bytes() // 4), dtype=torch.int32, device=d)
@@ -299,3 +362,29 @@ class GameBatch:
 
     def terminal(self):
         return self.games[:, L.CitGame.terminal.offset].to(torch.bool)
+
+
+def _merge_targets(main, extra, over):
+    """cfr_targets of the main pool (retried lanes empty) + those of a retry
+    sub-batch (sub lane i = global lane over[i]) -> one dict in lane order, CSR
+    option rows re-laid out in target order."""
+    d = main["meta"].device
+    over = over.to(d)
+    em = extra["meta"].clone()
+    em[:, 0] = over[em[:, 0].long()].to(em.dtype)
+    meta = torch.cat([main["meta"], em])
+    order = torch.sort(meta[:, 0].long() * (1 << 32) + torch.arange(meta.shape[0], device=d), stable=True).indices
+    meta = meta[order]
+    nc_main = main["dist"].shape[0]
+    first = torch.cat([main["meta"][:, 4].long(), extra["meta"][:, 4].long() + nc_main])[order]
+    nch = meta[:, 3].long()
+    new_first = torch.cumsum(nch, 0) - nch
+    rows = torch.repeat_interleave(first - new_first, nch) + torch.arange(int(nch.sum()), device=d)
+    dist = torch.cat([main["dist"], extra["dist"]])[rows]
+    opt_feat = torch.cat([main["opt_feat"], extra["opt_feat"]])[rows]
+    meta[:, 4] = new_first.to(meta.dtype)
+    counts = main["counts"].clone()
+    counts[over] = extra["counts"]
+    return {"meta": meta, "feat": torch.cat([main["feat"], extra["feat"]])[order],
+            "value": torch.cat([main["value"], extra["value"]])[order], "dist": dist, "opt_feat": opt_feat,
+            "counts": counts}

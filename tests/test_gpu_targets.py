@@ -101,3 +101,31 @@ def test_gpu_setup_game_golden():
         k, (lane, node, pid, nch, c0) = by_lane[l]
         check_targets([(feat[l], t["opt_feat"][c0:c0 + nch], t["value"][k], t["dist"][c0:c0 + nch])],
                       [r["result"]], r["seed"])
+
+
+def test_gpu_pool_overflow_retry():
+    """A tree that outgrows its node pool is searched again with a larger pool:
+    decisions, stats, streams and targets equal those of a run whose pool was
+    large enough from the start (reference behaviour has no pool at all)."""
+    from citadels_self_play_amd.engine import GameBatch
+    seeds = np.arange(7_100_000, 7_100_064)
+    out = []
+    for cap, retries in ((96, 3), (8192, 0)):
+        b = GameBatch(seeds, preset=True)
+        b.random_position(100)
+        b.seed_numpy()
+        chosen, stats = b.cfr_decide(500, node_cap=cap, max_retries=retries)
+        t = b.cfr_targets(stats[:, 0])
+        torch.cuda.synchronize()
+        out.append((chosen.cpu().numpy(), stats.cpu().numpy(), _split(t), b.rows(), b.mt.cpu().numpy(),
+                    b.mt_idx.cpu().numpy(), b.np_mt.cpu().numpy(), b.np_idx.cpu().numpy()))
+    small, big = out
+    assert (big[1][:, 4] == 0).all() and (small[1][:, 4] == 0).all()
+    assert (big[1][:, 1] > 96).sum() > 8            # most lanes did overflow the small pool
+    for x, y in zip(small[:2] + small[3:], big[:2] + big[3:]):
+        assert np.array_equal(x, y)
+    for a, bb in zip(small[2], big[2]):
+        assert len(a) == len(bb)
+        for x, y in zip(a, bb):
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v)

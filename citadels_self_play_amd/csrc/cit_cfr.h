@@ -650,7 +650,7 @@ CIT_NOINLINE void cfr_write_feat(CfrTree& T, int n, float* feat) {
   const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
   int pid = (T.nodes[n].flags & NF_ROLE_PICK) ? 5 : -1;
   CFR_SYNC();
-  if (CFR_LANE == 0) cit_encode_game(g, feat, pid);
+  cit_encode_game(g, feat, pid);   // the whole team (identical stores): the engine's scans are wave-wide
   CFR_SYNC();
 }
 

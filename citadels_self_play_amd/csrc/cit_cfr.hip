@@ -9,17 +9,9 @@
 
 namespace {
 
-__device__ __forceinline__ CitMT lane_mt(uint32_t* mt, const uint32_t* idx, int B, long l) {
-  CitMT r;
-  r.mt = mt + l;
-  r.stride = B;
-  r.pos = idx[l];
-  return r;
-}
-
 // The tree's two streams (CPython `random`, numpy `np.random`) live in LDS for
 // the whole launch: every draw of the search is an LDS access instead of a
-// strided HBM one.
+// strided HBM one, and a twist is done by the 64 lanes together.
 __device__ __forceinline__ CitMT mt_stage_in(uint32_t* dst, const uint32_t* mt, const uint32_t* idx, int B, long l) {
   for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) dst[i] = mt[(long)i * B + l];
   __syncthreads();
@@ -27,6 +19,7 @@ __device__ __forceinline__ CitMT mt_stage_in(uint32_t* dst, const uint32_t* mt, 
   r.mt = dst;
   r.stride = 1;
   r.pos = idx[l];
+  r.coop = 1;     // the team runs the search in lockstep: lane-parallel twist
   return r;
 }
 __device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, int B, long l) {
@@ -141,26 +134,6 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   }
 }
 
-__global__ void k_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
-                                   int32_t* counts) {
-  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= B) return;
-  CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
-  cfr_count_targets(T, roots[l], mode, counts[2 * l], counts[2 * l + 1]);
-}
-
-__global__ void k_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
-                              uint32_t* mt,
-                              uint32_t* idx, const int32_t* offsets, int32_t* meta, float* feat, double* value,
-                              double* dist, float* opt_feat) {
-  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= B) return;
-  CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
-  CitMT r = lane_mt(mt, idx, B, l);
-  cfr_emit_targets(T, r, roots[l], mode, (int)l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
-  idx[l] = r.pos;
-}
-
 }  // namespace
 
 #define CHECK_LAUNCH()                       \
@@ -185,25 +158,6 @@ int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt,
     return -1;
   hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
                      B, iters, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats);
-  CHECK_LAUNCH();
-}
-
-int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
-                         int32_t* counts, hipStream_t stream) {
-  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !counts || mode < 0 || mode > 1) return -1;
-  hipLaunchKernelGGL(k_cfr_target_count, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap,
-                     edge_cap, roots, mode, counts);
-  CHECK_LAUNCH();
-}
-
-int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode, uint32_t* mt,
-                    uint32_t* mt_idx, const int32_t* offsets, int32_t* meta, float* feat, double* value, double* dist,
-                    float* opt_feat, hipStream_t stream) {
-  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !mt || !mt_idx || !offsets || mode < 0 ||
-      mode > 1)
-    return -1;
-  hipLaunchKernelGGL(k_cfr_targets, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap, edge_cap,
-                     roots, mode, mt, mt_idx, offsets, meta, feat, value, dist, opt_feat);
   CHECK_LAUNCH();
 }
 

@@ -24,6 +24,27 @@
 #define CIT_HDI inline
 #endif
 
+// ------------------------------------------------------------ wave helpers
+// CIT_WAVE: device code in a translation unit whose engine callers run the
+// game on all 64 lanes of a wavefront with uniform control flow (every lane
+// computes the same values; cit_hip.hip's uniform kernels and the MCCFR
+// kernels).  The list scans of the engine then read one element per lane
+// (one LDS round trip instead of one per element) and combine with ballots
+// and readlanes; results are identical to the serial loops, which the host
+// build and the one-game-per-lane kernels (CIT_NO_WAVE units) keep.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CIT_NO_WAVE)
+#define CIT_WAVE 1
+__device__ __forceinline__ int cit_lane() { return (int)__lane_id(); }
+__device__ __forceinline__ uint64_t cit_ballot(bool p) { return (uint64_t)__ballot(p); }
+__device__ __forceinline__ int cit_readlane(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
+extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_or_u32(unsigned int);
+__device__ __forceinline__ uint64_t cit_wave_or64(uint64_t v) {
+  return ((uint64_t)__ockl_wfred_or_u32((unsigned int)(v >> 32)) << 32) | __ockl_wfred_or_u32((unsigned int)v);
+}
+#else
+#define CIT_WAVE 0
+#endif
+
 // ---------------------------------------------------------------- capacities
 #define CIT_NP 6
 #define CIT_HAND_CAP 32
@@ -187,6 +208,8 @@ struct CitMT {
   uint32_t* mt;
   int stride;
   uint32_t pos;   // 624 = twist next
+  int coop;       // device: every lane of the wave runs this stream's owner
+                  // uniformly, so the twist is done lane-parallel (stride 1)
 };
 
 CIT_HD uint32_t mt_word(const CitMT& r, int i) { return r.mt[(long)i * r.stride]; }
@@ -236,8 +259,10 @@ __device__ unsigned long long g_roll_prof[160];
 struct CitTwistProf {
   unsigned long long t0 = clock64();
   __device__ ~CitTwistProf() {
-    atomicAdd(&g_roll_prof[6], clock64() - t0);
-    atomicAdd(&g_roll_prof[7], 1ull);
+    if (__lane_id() == 0) {
+      atomicAdd(&g_roll_prof[6], clock64() - t0);
+      atomicAdd(&g_roll_prof[7], 1ull);
+    }
   }
 };
 #define CIT_TWIST_PROF() CitTwistProf _twist_prof
@@ -276,10 +301,46 @@ CIT_HDI CIT_TWIST_ATTR void mt_twist(const CitMT& r) {
 }
 static_assert(CIT_MT_N % CIT_TWIST_CHUNK == 0 && CIT_TWIST_CHUNK < 227, "twist chunking");
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// The twist by all 64 lanes of a wave that runs the stream's owner uniformly
+// (CitMT::coop), in place over an LDS block (stride 1).  New word i reads old
+// i, i+1 and (i+397) mod 624; the serial recurrence makes (i+397) mod 624 a
+// NEW word for i >= 227 and word 0 new for i = 623.  Hence three phases,
+// [0,227) from old words, [227,454) reading phase 1, [454,624) reading phase
+// 2 (and new word 0); within a phase every lane reads before any lane writes.
+typedef __attribute__((address_space(3))) uint32_t cit_lds_u32;
+__device__ __attribute__((noinline)) void mt_twist_coop(cit_lds_u32* m) {
+  CIT_TWIST_PROF();
+  const int ln = (int)__lane_id();
+  const int bounds[4] = {0, 227, 454, CIT_MT_N};
+#pragma unroll
+  for (int ph = 0; ph < 3; ph++) {
+    for (int i0 = bounds[ph]; i0 < bounds[ph + 1]; i0 += 64) {
+      int i = i0 + ln;
+      bool on = i < bounds[ph + 1];
+      uint32_t v = 0;
+      if (on) {
+        uint32_t y = (m[i] & 0x80000000u) | (m[i + 1 < CIT_MT_N ? i + 1 : 0] & 0x7fffffffu);
+        int k = i + 397;
+        v = m[k < CIT_MT_N ? k : k - CIT_MT_N] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      __syncthreads();
+      if (on) m[i] = v;
+      __syncthreads();
+    }
+  }
+}
+#endif
+
 CIT_HD uint32_t mt_next(CitMT& r) {
   uint32_t i = r.pos;
   if (i >= CIT_MT_N) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (r.coop) mt_twist_coop((cit_lds_u32*)r.mt);
+    else mt_twist(r);
+#else
     mt_twist(r);
+#endif
     i = 0;
   }
   uint32_t y = mt_word(r, (int)i);
@@ -291,11 +352,7 @@ CIT_HD uint32_t mt_next(CitMT& r) {
   return y;
 }
 
-CIT_HD int bit_length(uint32_t n) {
-  int k = 0;
-  while (n) { k++; n >>= 1; }
-  return k;
-}
+CIT_HD int bit_length(uint32_t n) { return n ? 32 - __builtin_clz(n) : 0; }
 
 // random._randbelow_with_getrandbits (Lib/random.py:239-249)
 CIT_HD uint32_t mt_randbelow(CitMT& r, uint32_t n) {

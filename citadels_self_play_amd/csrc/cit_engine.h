@@ -11,17 +11,37 @@
 #include "cit_core.h"
 
 // =========================================================== list helpers
+// Lists of up to 64 entries are scanned one element per lane under CIT_WAVE
+// (cit_core.h); longer ones (the deck ring) and the host build loop.
 CIT_HD bool has_type(const uint8_t* a, int n, int t) {
+#if CIT_WAVE
+  if (n <= 64) {
+    int i = cit_lane();
+    return cit_ballot(i < n && card_type(a[i]) == t) != 0;
+  }
+#endif
   for (int i = 0; i < n; i++)
     if (card_type(a[i]) == t) return true;
   return false;
 }
 CIT_HD int count_type(const uint8_t* a, int n, int t) {
+#if CIT_WAVE
+  if (n <= 64) {
+    int i = cit_lane();
+    return __popcll(cit_ballot(i < n && card_type(a[i]) == t));
+  }
+#endif
   int k = 0;
   for (int i = 0; i < n; i++) k += card_type(a[i]) == t;
   return k;
 }
 CIT_HD int count_suit(const uint8_t* a, int n, int s) {
+#if CIT_WAVE
+  if (n <= 64) {
+    int i = cit_lane();
+    return __popcll(cit_ballot(i < n && card_suit(a[i]) == s));
+  }
+#endif
   int k = 0;
   for (int i = 0; i < n; i++) k += card_suit(a[i]) == s;
   return k;
@@ -30,6 +50,20 @@ CIT_HD int count_suit(const uint8_t* a, int n, int s) {
 // returns it, or c itself when there is none.
 CIT_HD int take_like(uint8_t* a, uint8_t& n, int c) {
   int t = card_type(c);
+#if CIT_WAVE
+  int cnt = n;
+  if (cnt <= 64) {
+    int j = cit_lane();
+    int v = j < cnt ? a[j] : CIT_NO_CARD;
+    uint64_t m = cit_ballot(j < cnt && card_type(v) == t);
+    if (!m) return c;
+    int i = __ffsll((unsigned long long)m) - 1;
+    int r = cit_readlane(v, i);
+    if (j > i && j < cnt) a[j - 1] = (uint8_t)v;   // every lane loaded before any stores
+    n = (uint8_t)(cnt - 1);
+    return r;
+  }
+#endif
   for (int i = 0; i < n; i++) {
     if (card_type(a[i]) == t) {
       int r = a[i];
@@ -48,11 +82,35 @@ CIT_HD void put_card(CitGame& g, uint8_t* a, uint8_t& n, int cap, int c) {
 }
 CIT_HD int pop_front(uint8_t* a, uint8_t& n) {
   if (!n) return CIT_NO_CARD;
+#if CIT_WAVE
+  int cnt = n;
+  if (cnt <= 64) {
+    int j = cit_lane();
+    int v = j < cnt ? a[j] : 0;
+    int r = cit_readlane(v, 0);
+    if (j >= 1 && j < cnt) a[j - 1] = (uint8_t)v;
+    n = (uint8_t)(cnt - 1);
+    return r;
+  }
+#endif
   int r = a[0];
   for (int j = 1; j < n; j++) a[j - 1] = a[j];
   n--;
   return r;
 }
+// Read-only view of a list of up to 64 bytes for a serial loop: under
+// CIT_WAVE lane i holds a[i] (one LDS round trip) and [i] is a readlane.
+struct ByteList {
+#if CIT_WAVE
+  int v;
+  CIT_HD ByteList(const uint8_t* a, int n) { int i = cit_lane(); v = i < n ? a[i] : 0; }
+  CIT_HD int operator[](int i) const { return cit_readlane(v, i); }
+#else
+  const uint8_t* a;
+  CIT_HD ByteList(const uint8_t* p, int) : a(p) {}
+  CIT_HD int operator[](int i) const { return a[i]; }
+#endif
+};
 
 #define HAND(p) (p).hand, (p).n_hand, CIT_HAND_CAP
 #define BUILD(p) (p).build, (p).n_build, CIT_BUILD_CAP
@@ -61,6 +119,12 @@ CIT_HD int pop_front(uint8_t* a, uint8_t& n) {
 CIT_HD bool p_has(const CitPlayer& p, int t) { return has_type(p.build, p.n_build, t); }
 // bit t set iff a card of type t is in the list
 CIT_HD uint64_t type_mask(const uint8_t* a, int n) {
+#if CIT_WAVE
+  if (n <= 64) {
+    int i = cit_lane();
+    return cit_wave_or64(i < n ? 1ull << card_type(a[i]) : 0ull);
+  }
+#endif
   uint64_t m = 0;
   for (int i = 0; i < n; i++) m |= 1ull << card_type(a[i]);
   return m;
@@ -195,6 +259,13 @@ CIT_HD int role_of_id(const CitGame& g, int rid) { return rid < 0 ? ROLE_BEWITCH
 // get_player_from_role_id (game.py:403-412); -1 for None
 CIT_HD int holder(const CitGame& g, int rid) {
   int want = role_of_id(g, rid);
+#if CIT_WAVE
+  {
+    int i = cit_lane();
+    uint64_t m = cit_ballot(i < CIT_NP && g.pl[i < CIT_NP ? i : 0].role == want);
+    return m ? __ffsll((unsigned long long)m) - 1 : -1;
+  }
+#endif
   for (int i = 0; i < CIT_NP; i++)
     if (g.pl[i].role == want) return i;
   return -1;
@@ -405,6 +476,12 @@ CIT_HD int check_game_ending(CitGame& g) {
 // is_last_round (game.py:173-181)
 CIT_HD void is_last_round(CitGame& g) {
   if (g.ending) return;
+#if CIT_WAVE
+  {
+    int i = cit_lane();
+    if (!cit_ballot(i < CIT_NP && g.pl[i < CIT_NP ? i : 0].n_build == 7)) return;
+  }
+#endif
   for (int i = 0; i < CIT_NP; i++)
     if (g.pl[i].n_build == 7) {
       g.ending = 1;

@@ -12,35 +12,23 @@
 
 #include "../../include/citadels.h"
 #include "cit_engine.h"
+#include "cit_lanes.h"
 
 static_assert(sizeof(CitOpt) == sizeof(CitOption), "descriptor layouts differ");
 
 #define ROW_W (CIT_GAME_BYTES / 4)
-#define LDS_W (ROW_W + 1)
-#define MAX_G 64
 #ifndef ROLLOUT_BUF
 #define ROLLOUT_BUF 32
 #endif
 
 namespace {
 
-__device__ __forceinline__ void stage_in(uint32_t* lds, const uint32_t* __restrict__ gm, long g0, int nrows) {
-  for (int i = threadIdx.x; i < nrows * ROW_W; i += blockDim.x) {
-    int r = i / ROW_W, w = i - r * ROW_W;
-    lds[r * LDS_W + w] = gm[(g0 + r) * ROW_W + w];
-  }
-}
-__device__ __forceinline__ void stage_out(const uint32_t* lds, uint32_t* __restrict__ gm, long g0, int nrows) {
-  for (int i = threadIdx.x; i < nrows * ROW_W; i += blockDim.x) {
-    int r = i / ROW_W, w = i - r * ROW_W;
-    gm[(g0 + r) * ROW_W + w] = lds[r * LDS_W + w];
-  }
-}
 __device__ __forceinline__ CitMT lane_mt(uint32_t* mt, const uint32_t* idx, int B, long l) {
   CitMT r;
   r.mt = mt + l;
   r.stride = B;
   r.pos = idx[l];
+  r.coop = 0;
   return r;
 }
 
@@ -49,7 +37,14 @@ __device__ __forceinline__ CitMT lane_mt(uint32_t* mt, const uint32_t* idx, int 
 // SGPRs and branches with s_cbranch instead of exec masks (measured: +27 %
 // transitions/s at B = 4096 over one game per lane, and no scratch spills).
 // The 64 lanes stage the row (and, for multi-step kernels, the 624 MT19937
-// words) into LDS; lane 0 runs `body(game, stream, l)`; the lanes write back.
+// words) into LDS and run `body(game, stream, l)` together: every lane
+// computes the same values (LDS reads at uniform addresses are uniform), so
+// control flow never diverges, and the lanes are there for lane-parallel
+// pieces such as the MT19937 twist (CitMT::coop).  CIT_LANE0_BODY restores
+// the lane-0-only body for A/B runs.  The lanes then write back.
+#ifndef CIT_LANE0_BODY
+#define CIT_LANE0_BODY 0
+#endif
 template <bool MT_LDS, bool STAGE_ROW, class F>
 __device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, F&& body) {
   __shared__ __attribute__((aligned(16))) uint32_t row[ROW_W];
@@ -60,7 +55,7 @@ __device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint
   if (MT_LDS)
     for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) mts[i] = mt[(long)i * B + l];
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (!CIT_LANE0_BODY || threadIdx.x == 0) {
     CitGame& g = *reinterpret_cast<CitGame*>(row);
     CitMT r;
     if (MT_LDS) {
@@ -71,8 +66,9 @@ __device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint
       r.stride = B;
     }
     r.pos = idx[l];
+    r.coop = MT_LDS && !CIT_LANE0_BODY;
     body(g, r, l);
-    idx[l] = r.pos;
+    if (threadIdx.x == 0) idx[l] = r.pos;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < ROW_W; i += blockDim.x) games[l * ROW_W + i] = row[i];
@@ -153,37 +149,6 @@ __global__ void k_random_choice(uint32_t* games, uint32_t* mt, uint32_t* idx, in
   chosen[l] = opts[l * max_opts + k];
 }
 
-// The step loop with G games per wavefront, one per lane (games_per_block =
-// G > 0; kept for sweeps: divergence across a 47-way option switch makes it
-// slower than k_rollout_u at every B measured).  Rows in LDS at an odd-dword
-// stride, MT19937 words in HBM (structure of arrays).
-__global__ void k_rollout(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_steps,
-                          int32_t* steps_out, int32_t* winner) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  long g0 = (long)blockIdx.x * blockDim.x;
-  int nrows = (int)min((long)blockDim.x, (long)B - g0);
-  stage_in(lds, games, g0, nrows);
-  __syncthreads();
-  if (threadIdx.x < nrows) {
-    long l = g0 + threadIdx.x;
-    CitGame& g = *reinterpret_cast<CitGame*>(lds + threadIdx.x * LDS_W);
-    CitMT r = lane_mt(mt, idx, B, l);
-    uint64_t* sc = seer + l * CIT_SEER_MAX;
-    int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
-    int s = 0;
-    while (!g.terminal && !g.err && s < cap) {
-      cit_random_step(g, r, sc);
-      s++;
-    }
-    if (max_steps < 0 && s >= cap && !g.terminal && !g.err) g.err |= CIT_ERR_STEP_CAP;
-    steps_out[l] += s;
-    winner[l] = g.winner;
-    idx[l] = r.pos;
-  }
-  __syncthreads();
-  stage_out(lds, games, g0, nrows);
-}
-
 #ifdef CIT_PROF_ROLLOUT
 // Phase cycle accounting of the rollout step (profiling builds only:
 // tools/prof_rollout.py).  [0..4] prepare / enumerate / randbelow / pick /
@@ -229,7 +194,8 @@ __global__ __launch_bounds__(64) void k_rollout_u(uint32_t* games, uint32_t* mt,
       prof_step(g, r, sc, buf, ROLLOUT_BUF, acc);
       s++;
     }
-    for (int i = 0; i < 160; i++) atomicAdd(&g_roll_prof[i], acc[i]);
+    if (threadIdx.x == 0)
+      for (int i = 0; i < 160; i++) atomicAdd(&g_roll_prof[i], acc[i]);
 #else
     while (!g.terminal && !g.err && s < cap) {
       if (ROLLOUT_BUF) cit_random_step_buf(g, r, sc, buf, ROLLOUT_BUF);
@@ -283,20 +249,6 @@ __global__ __launch_bounds__(64) void k_close_position(uint32_t* games, uint32_t
   uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     index[l] = cit_close_position(g, r, seer + l * CIT_SEER_MAX, store + l * (long)CIT_CLOSE_ROWS * ROW_W);
   });
-}
-
-template <class K>
-int set_lds(K kernel, size_t bytes) {
-  return (int)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-}
-size_t lds_bytes(int G) { return (size_t)G * LDS_W * 4; }
-
-bool g_attrs_done = false;
-int ensure_attrs() {
-  if (g_attrs_done) return 0;
-  int e = set_lds(k_rollout, lds_bytes(MAX_G));
-  if (!e) g_attrs_done = true;
-  return e;
 }
 
 }  // namespace
@@ -385,19 +337,15 @@ int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitO
 int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
                        int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream) {
   if (B <= 0 || !games || !mt || !mt_idx || !seer || !steps || !winner) return -1;
-  if (games_per_block > MAX_G) return -1;
-  if (int e = ensure_attrs()) return e;
+  if (games_per_block > CIT_LANES_MAX_G) return -1;
   // 0 = auto: one game per workgroup, wave-uniform code (k_rollout_u)
   if (games_per_block <= 0) {
     hipLaunchKernelGGL(k_rollout_u, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, seer, B, max_steps,
                        steps, winner);
     CHECK_LAUNCH();
   }
-  // G lanes = G games per workgroup (one wavefront), per-lane code
-  int G = games_per_block;
-  hipLaunchKernelGGL(k_rollout, dim3((B + G - 1) / G), dim3(G), lds_bytes(G), stream, (uint32_t*)games, mt, mt_idx,
-                     seer, B, max_steps, steps, winner);
-  CHECK_LAUNCH();
+  // G lanes = G games per workgroup (one wavefront), per-lane code (cit_lanes.hip)
+  return cit_rollout_lanes((uint32_t*)games, mt, mt_idx, seer, B, max_steps, games_per_block, steps, winner, stream);
 }
 
 int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int lo, int hi,

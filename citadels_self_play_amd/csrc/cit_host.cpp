@@ -39,6 +39,7 @@ static CitMT lane_rng(uint32_t* mt, uint32_t* idx, int B, int l) {
   r.mt = mt + l;
   r.stride = B;
   r.pos = idx[l];
+  r.coop = 0;
   return r;
 }
 #define SAVE(r) idx[l] = (r).pos

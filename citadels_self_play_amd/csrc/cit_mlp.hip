@@ -9,6 +9,8 @@
 // starting from 0, then + bias, then ReLU), activations staged in LDS,
 // weights pre-transposed to [k][n] so a half-wave reads 128 contiguous bytes.
 // fc4 (6 outputs) runs as one padded 32-column tile.
+// One row per lane (the featurizer kernels): no wave-uniform engine scans.
+#define CIT_NO_WAVE 1
 #include <hip/hip_runtime.h>
 
 #include "../../include/citadels.h"

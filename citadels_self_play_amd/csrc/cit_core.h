@@ -209,8 +209,16 @@ struct CitMT {
   int stride;
   uint32_t pos;   // 624 = twist next
   int coop;       // device: every lane of the wave runs this stream's owner
-                  // uniformly, so the twist is done lane-parallel (stride 1)
+                  // uniformly, so the twist is done lane-parallel (stride 1);
+                  // CIT_MT_WINDOW: also draw through `win` (below)
+  // CIT_MT_WINDOW streams (a CitMT held in registers, never in memory): lane
+  // i of `win` holds the TEMPERED word win_base + i, so a draw is a readlane
+  // and the LDS block is read once per 64 draws (all lanes at once).
+  uint32_t win;
+  int win_base;   // -1: empty
 };
+#define CIT_MT_COOP 1
+#define CIT_MT_WINDOW 2
 
 CIT_HD uint32_t mt_word(const CitMT& r, int i) { return r.mt[(long)i * r.stride]; }
 CIT_HD void mt_set(const CitMT& r, int i, uint32_t v) { r.mt[(long)i * r.stride] = v; }
@@ -332,24 +340,42 @@ __device__ __attribute__((noinline)) void mt_twist_coop(cit_lds_u32* m) {
 }
 #endif
 
-CIT_HD uint32_t mt_next(CitMT& r) {
-  uint32_t i = r.pos;
-  if (i >= CIT_MT_N) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (r.coop) mt_twist_coop((cit_lds_u32*)r.mt);
-    else mt_twist(r);
-#else
-    mt_twist(r);
-#endif
-    i = 0;
-  }
-  uint32_t y = mt_word(r, (int)i);
-  r.pos = i + 1;
+CIT_HD uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680u;
   y ^= (y << 15) & 0xefc60000u;
   y ^= (y >> 18);
   return y;
+}
+
+CIT_HD uint32_t mt_next(CitMT& r) {
+  uint32_t i = r.pos;
+  if (i >= CIT_MT_N) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (r.coop) {
+      mt_twist_coop((cit_lds_u32*)r.mt);
+      r.win_base = -1;
+    } else {
+      mt_twist(r);
+    }
+#else
+    mt_twist(r);
+#endif
+    i = 0;
+  }
+  r.pos = i + 1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (r.coop == CIT_MT_WINDOW) {
+    int b = (int)(i & ~63u);
+    if (b != r.win_base) {
+      int j = b + (int)__lane_id();
+      r.win = mt_temper(j < CIT_MT_N ? ((const cit_lds_u32*)r.mt)[j] : 0u);
+      r.win_base = b;
+    }
+    return (uint32_t)__builtin_amdgcn_readlane((int)r.win, (int)(i & 63u));
+  }
+#endif
+  return mt_temper(mt_word(r, (int)i));
 }
 
 CIT_HD int bit_length(uint32_t n) { return n ? 32 - __builtin_clz(n) : 0; }

@@ -348,8 +348,19 @@ CIT_HD void setup_next_player(CitGame& g, int current) {
     g.gs_state = 1;
     int r = role_rank(g, g.pl[current].role);
     int i = -1;
+#if CIT_WAVE
+    {
+      int k = cit_lane(), nu = g.n_used_roles;
+      uint64_t m = cit_ballot(k < nu && k < CIT_NP && g.used_roles[k < CIT_NP ? k : 0] == r);
+      if (nu <= CIT_NP) i = m ? __ffsll((unsigned long long)m) - 1 : -1;
+      else
+        for (int kk = 0; kk < nu; kk++)
+          if (g.used_roles[kk] == r) { i = kk; break; }
+    }
+#else
     for (int k = 0; k < g.n_used_roles; k++)
       if (g.used_roles[k] == r) { i = k; break; }
+#endif
     if (i < 0) { g.err |= CIT_ERR_VALUE; return; }
     if (i + 1 >= g.n_used_roles) { g.err |= CIT_ERR_INDEX; return; }
     g.gs_pid = (int8_t)holder_checked(g, g.used_roles[i + 1]);
@@ -369,6 +380,20 @@ CIT_HD void cit_setup_round(CitGame& g, CitMT& rng) {
   for (int r = 0; r < 7; r++) m |= (uint8_t)(1u << pool[r]);   // pool[7] is the face-down role
   g.rtc = m;
   int c = -1;
+#if CIT_WAVE
+  {
+    int i = cit_lane();
+    uint64_t m = cit_ballot(i < CIT_NP && (g.pl[i < CIT_NP ? i : 0].flags & PF_CROWN));
+    c = m ? __ffsll((unsigned long long)m) - 1 : -1;
+    if (c < 0) { g.err |= CIT_ERR_UNSUPPORTED; return; }
+    int v = i < CIT_NP ? g.turn[(i + c) % CIT_NP] : 0;    // every lane reads before any lane writes
+    if (i < CIT_NP) g.turn[i] = (uint8_t)v;
+    gs_fresh(g, 0, cit_readlane(v, 0));
+    kh_decay(g);
+    if (i < CIT_NP * CIT_NP) g.pl[i / CIT_NP].kr[i % CIT_NP] = 0;
+    return;
+  }
+#endif
   for (int i = 0; i < CIT_NP; i++)
     if (g.pl[i].flags & PF_CROWN) { c = i; break; }
   if (c < 0) { g.err |= CIT_ERR_UNSUPPORTED; return; }     // turn order would double (game.py:164-165)
@@ -506,6 +531,52 @@ CIT_HD CitOpt mk(int name, int perp, int target = -1, int a = 0, int b = 0, int 
 }
 enum { OF_TUPLE = 1, OF_NEXT_WITCH = 1, OF_CROWN = 2, OF_BUILD = 1, OF_FACTORY = 1 };
 
+#if CIT_WAVE
+// Lane-parallel generation (CIT_WAVE): every lane proposes one option (p, o);
+// the proposals are taken in lane order, i.e. lane i plays iteration i of
+// the reference's loop.  cit_lane_rank = number of proposing lanes below.
+__device__ __forceinline__ int cit_lane_rank(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+__device__ __forceinline__ CitOpt cit_readlane_opt(const CitOpt& o, int src) {
+  uint32_t w[4];
+  __builtin_memcpy(w, &o, 16);
+  for (int j = 0; j < 4; j++) w[j] = (uint32_t)__builtin_amdgcn_readlane((int)w[j], src);
+  CitOpt r;
+  __builtin_memcpy(&r, w, 16);
+  return r;
+}
+// true on the lowest valid lane of each key (the reference's `seen` sets:
+// first occurrence wins).  All lanes must be active.
+__device__ __forceinline__ bool cit_first_key(bool valid, int key) {
+  uint64_t m = cit_ballot(valid);
+  int me = cit_lane();
+  bool dup = false;
+  while (m) {
+    int j = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    if (j >= me) break;
+    dup |= key == __builtin_amdgcn_readlane(key, j);
+  }
+  return valid && !dup;
+}
+// list sinks: proposals compacted into buf[n + rank]
+#define CIT_WAVE_LIST_EMIT                                        \
+  CIT_HD bool wave_emit(bool p, const CitOpt& o) {                \
+    uint64_t m = cit_ballot(p);                                   \
+    int r = n + cit_lane_rank(m);                                 \
+    if (p && r < cap) buf[r] = o;                                 \
+    n += __popcll(m);                                             \
+    return false;                                                 \
+  }
+#else
+#define CIT_WAVE_LIST_EMIT
+#endif
+#define WEMIT(p, o)                                \
+  do {                                             \
+    if (s.wave_emit((p), (o))) return true;        \
+  } while (0)
+
 // Sinks: emit() returns true to stop the enumeration.
 // PickSink(k) stops at the k-th option (out); PickSink(-1) just counts (n).
 // The fused rollout uses this one sink for both passes, so the enumerator is
@@ -525,6 +596,20 @@ struct PickSink {
     n += cnt;
     return false;
   }
+#if CIT_WAVE
+  CIT_HD bool wave_emit(bool p, const CitOpt& o) {
+    uint64_t m = cit_ballot(p);
+    int c = __popcll(m);
+    if (k >= n && k < n + c) {
+      uint64_t hit = cit_ballot(p && cit_lane_rank(m) == k - n);
+      out = cit_readlane_opt(o, __ffsll((unsigned long long)hit) - 1);
+      n = k + 1;
+      return true;
+    }
+    n += c;
+    return false;
+  }
+#endif
 };
 struct ListSink {
   CitOpt* buf;
@@ -543,6 +628,7 @@ struct ListSink {
     n += cnt;
     return false;
   }
+  CIT_WAVE_LIST_EMIT
 };
 // The step loop's sink: lists the first `cap` options into `buf` (LDS in the
 // rollout kernel) while counting all of them.
@@ -563,6 +649,7 @@ struct BufSink {
     n += cnt;
     return false;
   }
+  CIT_WAVE_LIST_EMIT
 };
 
 #define EMIT(...)                                  \
@@ -610,6 +697,21 @@ CIT_HD bool gen_builds(const CitGame& g, int a, uint64_t bm, S& s) {
   int done = g.gs_adm[ADM_NON_TRADE] + (P.role == R_TRADER ? 0 : g.gs_adm[ADM_TRADE]);
   if (done >= lim) return false;
   bool factory = HAS(bm, 35);
+#if CIT_WAVE
+  {
+    int i = cit_lane(), nh = P.n_hand, gold = P.gold, reps = P.replicas;
+    int c = 0, t = 0;
+    bool q = false;
+    if (i < nh) {
+      c = P.hand[i];
+      t = card_type(c);
+      q = card_cost(c) + (factory && card_suit(c) == SUIT_UNIQUE ? 1 : 0) <= gold;
+    }
+    int rep = (HAS(bm, t) && !reps) ? reps + 1 : 0;
+    WEMIT(cit_first_key(q, t), mk(O_BUILD, a, -1, c, 0, rep));
+    return false;
+  }
+#endif
   uint64_t seen = 0;
   for (int i = 0; i < P.n_hand; i++) {
     int c = P.hand[i], t = card_type(c);
@@ -641,6 +743,10 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
   const CitPlayer& P = g.pl[a];
   switch (P.role) {
     case R_ASSASSIN:
+#if CIT_WAVE
+      WEMIT(cit_lane() >= 1 && cit_lane() < 8, mk(O_ASSASSINATION, a, -1, cit_lane()));
+      return false;
+#endif
       for (int r = 1; r < 8; r++) EMIT(mk(O_ASSASSINATION, a, -1, r));
       return false;
     case R_MAGISTRATE:
@@ -650,6 +756,10 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
             if (r != f0 && r != f1) EMIT(mk(O_MAGISTRATE_WARRANT, a, -1, r, f0, f1));
       return false;
     case R_THIEF:
+#if CIT_WAVE
+      WEMIT(cit_lane() >= 2 && cit_lane() < 8, mk(O_STEAL, a, -1, cit_lane()));
+      return false;
+#endif
       for (int r = 2; r < 8; r++) EMIT(mk(O_STEAL, a, -1, r));
       return false;
     case R_BLACKMAILER: {
@@ -668,6 +778,13 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
       return false;
     }
     case R_SPY:
+#if CIT_WAVE
+      {
+        int i = cit_lane(), p = i / 5;
+        WEMIT(i < 5 * CIT_NP && p != a, mk(O_SPY, a, p, i - 5 * p));
+        return false;
+      }
+#endif
       for (int p = 0; p < CIT_NP; p++)
         if (p != a)
           for (int su = 0; su < 5; su++) EMIT(mk(O_SPY, a, p, su));
@@ -685,6 +802,13 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
       return false;
     }
     case R_WIZARD:
+#if CIT_WAVE
+      {
+        int p = cit_lane();
+        WEMIT(p < CIT_NP && p != a && g.pl[p < CIT_NP ? p : 0].n_hand > 0, mk(O_LOOK_AT_HAND, a, p));
+        return false;
+      }
+#endif
       for (int p = 0; p < CIT_NP; p++)
         if (p != a && g.pl[p].n_hand > 0) EMIT(mk(O_LOOK_AT_HAND, a, p));
       return false;
@@ -759,6 +883,20 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
       for (int p = 0; p < CIT_NP; p++) {
         const CitPlayer& Q = g.pl[p];
         if (Q.n_build >= 7 || Q.role == R_BISHOP) continue;
+#if CIT_WAVE
+        {
+          int i = cit_lane(), nb = Q.n_build, gold = P.gold;
+          int b = 0, t = 0;
+          bool q = false;
+          if (i < nb) {
+            b = Q.build[i];
+            t = card_type(b);
+            q = card_cost(b) - 1 <= gold && t != 17;
+          }
+          WEMIT(cit_first_key(q, t), mk(O_WARLORD, a, p, b));
+          continue;
+        }
+#endif
         uint64_t seen = 0;
         for (int i = 0; i < Q.n_build; i++) {
           int b = Q.build[i], t = card_type(b);
@@ -824,13 +962,31 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
     EMIT(mk(O_TAKE_GOLD_WAR, a));
   if (HAS(bm, 21) && P.gold >= 2 && !g.gs_adm[ADM_SMITHY]) EMIT(mk(O_SMITHY, a));
   if (HAS(bm, 22) && !g.gs_adm[ADM_LAB])
+#if CIT_WAVE
+  {
+    int i = cit_lane(), nh = P.n_hand;
+    WEMIT(i < nh, mk(O_LAB, a, -1, i < nh ? P.hand[i] : 0));
+  }
+#else
     for (int i = 0; i < P.n_hand; i++) EMIT(mk(O_LAB, a, -1, P.hand[i]));
+#endif
   if (!g.gs_adm[ADM_MAGIC_SCHOOL] && HAS(bm, 25))
+#if CIT_WAVE
+    WEMIT(cit_lane() < 5, mk(O_MAGIC_SCHOOL, a, -1, cit_lane()));
+#else
     for (int su = 0; su < 5; su++) EMIT(mk(O_MAGIC_SCHOOL, a, -1, su));
+#endif
   if (HAS(bm, 27))
     for (int p = 0; p < CIT_NP; p++)
       if (p != a)
+#if CIT_WAVE
+      {
+        int i = cit_lane(), nb = g.pl[p].n_build;
+        WEMIT(i < nb, mk(O_WEAPON_STORAGE, a, p, i < nb ? g.pl[p].build[i] : 0));
+      }
+#else
         for (int i = 0; i < g.pl[p].n_build; i++) EMIT(mk(O_WEAPON_STORAGE, a, p, g.pl[p].build[i]));
+#endif
   if (HAS(bm, 29) && (P.flags & PF_LIGHTHOUSE)) {
     uint64_t seen = 0;
     for (int i = 0; i < g.n_deck; i++) {
@@ -842,6 +998,11 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
     }
   }
   if (HAS(bm, 34) && !g.gs_adm[ADM_MUSEUM]) {
+#if CIT_WAVE
+    int i = cit_lane(), nh = P.n_hand;
+    int c = i < nh ? P.hand[i] : 0;
+    WEMIT(cit_first_key(i < nh, card_type(c)), mk(O_MUSEUM, a, -1, c));
+#else
     uint64_t seen = 0;
     for (int i = 0; i < P.n_hand; i++) {
       int c = P.hand[i], t = card_type(c);
@@ -850,6 +1011,7 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
         EMIT(mk(O_MUSEUM, a, -1, c));
       }
     }
+#endif
   }
   EMIT(mk(O_FINISH_ROUND, a));
   return false;
@@ -900,6 +1062,10 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
   const CitPlayer& P = g.pl[a];
   int st = g.gs_state;
   if (st == 0) {
+#if CIT_WAVE
+    WEMIT(cit_lane() < 8 && ((g.rtc >> cit_lane()) & 1), mk(O_ROLE_PICK, a, -1, cit_lane()));
+    return false;
+#endif
     for (int r = 0; r < 8; r++)
       if ((g.rtc >> r) & 1) EMIT(mk(O_ROLE_PICK, a, -1, r));
     return false;
@@ -920,6 +1086,11 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
           for (int i = 0; i < P.n_jd; i++)
             for (int j = i + 1; j < P.n_jd; j++) EMIT(mk(O_WHICH_CARD, a, -1, P.jd[i], P.jd[j], 0, OF_TUPLE));
         } else {
+#if CIT_WAVE
+          int i = cit_lane(), nj = P.n_jd;
+          int c = i < nj ? P.jd[i] : 0;
+          WEMIT(cit_first_key(i < nj, card_type(c)), mk(O_WHICH_CARD, a, -1, c, CIT_NO_CARD));
+#else
           uint64_t seen = 0;
           for (int i = 0; i < P.n_jd; i++) {
             int t = card_type(P.jd[i]);
@@ -928,6 +1099,7 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
               EMIT(mk(O_WHICH_CARD, a, -1, P.jd[i], CIT_NO_CARD));
             }
           }
+#endif
         }
         return false;
       case 3:
@@ -953,7 +1125,11 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
         break;
     }
     if (role == R_WITCH) {
+#if CIT_WAVE
+      WEMIT(cit_lane() >= 1 && cit_lane() < 8, mk(O_BEWITCHING, a, -1, cit_lane()));
+#else
       for (int r = 1; r < 8; r++) EMIT(mk(O_BEWITCHING, a, -1, r));
+#endif
       return false;
     }
     if (bew) { s.err |= CIT_ERR_KEY; return true; }
@@ -1065,6 +1241,10 @@ CIT_HD CitOpt cit_pick_option(const CitGame& g, int k, const uint64_t* seer) {
 CIT_HD void confirm_roles(CitGame& g, int q) {
   int rq = role_rank(g, g.pl[q].role);
   uint16_t v = (uint16_t)((1u << (rq + 1)) | KR_CONFIRMED);
+#if CIT_WAVE
+  if (cit_lane() < CIT_NP) g.pl[cit_lane()].kr[q] = v;
+  return;
+#endif
   for (int p = 0; p < CIT_NP; p++) g.pl[p].kr[q] = v;
 }
 // move_crown + troneroom_owner_gold (option_functions.py:588-595,625-631)
@@ -1165,6 +1345,20 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       g.rtc &= (uint8_t)~(1u << rk);
       uint16_t rtc_mask = (uint16_t)(g.rtc << 1);
       uint16_t before = (uint16_t)(0x1FE & ~rtc_mask & ~(1u << (rk + 1)));
+#if CIT_WAVE
+      {
+        // turn_orders_for_roles is a permutation: one lane per seat
+        int i = cit_lane();
+        int p = i < CIT_NP ? g.turn[i] : 0;
+        uint64_t at = cit_ballot(i < CIT_NP && p == a);
+        int pos_a = at ? 63 - __clzll((long long)at) : 0;   // the last match, as the loop's
+        if (i < CIT_NP && p != a) P.kr[p] = (uint16_t)((P.kr[p] & KR_CONFIRMED) | (i < pos_a ? before : rtc_mask));
+        int last = cit_readlane(p, CIT_NP - 1);
+        if (a != last) gs_set(g, 0, cit_readlane(p, pos_a + 1 < CIT_NP ? pos_a + 1 : 0));
+        else setup_next_player(g, -1);
+        break;
+      }
+#endif
       int pos_a = 0;
       for (int i = 0; i < CIT_NP; i++)
         if (g.turn[i] == a) pos_a = i;

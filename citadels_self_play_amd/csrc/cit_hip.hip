@@ -66,7 +66,9 @@ __device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint
       r.stride = B;
     }
     r.pos = idx[l];
-    r.coop = MT_LDS && !CIT_LANE0_BODY;
+    r.coop = MT_LDS && !CIT_LANE0_BODY ? CIT_MT_WINDOW : 0;
+    r.win = 0;
+    r.win_base = -1;
     body(g, r, l);
     if (threadIdx.x == 0) idx[l] = r.pos;
   }

@@ -131,6 +131,27 @@ CIT_HD uint64_t type_mask(const uint8_t* a, int n) {
 }
 #define HAS(mask, t) (((mask) >> (t)) & 1)
 
+// the first seat whose buildings hold type t, or -1 (the reference's seat
+// loops over p_has: get_graveyard_owner, troneroom_owner_gold).  Wave: lane l
+// reads building l % 10 of seat l / 10 (a seat with more than 10 buildings
+// falls back to the loop).
+CIT_HD int seat_with_type(const CitGame& g, int t) {
+#if CIT_WAVE
+  {
+    int l = cit_lane(), p = l / 10, i = l - 10 * p, ps = p < CIT_NP ? p : 0;
+    int nb = g.pl[ps].n_build;
+    int c = g.pl[ps].build[i];
+    if (!cit_ballot(i == 0 && p < CIT_NP && nb > 10)) {
+      uint64_t m = cit_ballot(p < CIT_NP && i < nb && card_type(c) == t);
+      return m ? (__ffsll((unsigned long long)m) - 1) / 10 : -1;
+    }
+  }
+#endif
+  for (int p = 0; p < CIT_NP; p++)
+    if (p_has(g.pl[p], t)) return p;
+  return -1;
+}
+
 // ------------------------------------------------------------ deck (ring)
 CIT_HD int deck_at(const CitGame& g, int i) { return g.deck[(g.deck_head + i) & (CIT_DECK_CAP - 1)]; }
 CIT_HD uint8_t& deck_ref(CitGame& g, int i) { return g.deck[(g.deck_head + i) & (CIT_DECK_CAP - 1)]; }
@@ -185,6 +206,22 @@ CIT_HD void reshuffle_if_empty(CitGame& g, CitMT& rng) {
   g.n_discard = 0;
 }
 CIT_HD void draw_into(CitGame& g, CitMT& rng, uint8_t* a, uint8_t& n, int cap, int k) {
+#if CIT_WAVE
+  {
+    // enough cards in the deck (no reshuffle) and room in the list: the k
+    // front cards move in one load + one store by k lanes
+    int nd = g.n_deck, head = g.deck_head, na = n;
+    if (k <= 64 && nd >= k && na + k <= cap) {
+      int l = cit_lane();
+      int c = g.deck[(head + l) & (CIT_DECK_CAP - 1)];
+      if (l < k) a[na + l] = (uint8_t)c;
+      n = (uint8_t)(na + k);
+      g.deck_head = (uint8_t)((head + k) & (CIT_DECK_CAP - 1));
+      g.n_deck = (uint8_t)(nd - k);
+      return;
+    }
+  }
+#endif
   for (int i = 0; i < k; i++) {
     reshuffle_if_empty(g, rng);
     put_card(g, a, n, cap, deck_draw(g));
@@ -206,11 +243,48 @@ CIT_HD void kh_append(CitGame& g, int owner, int target, int conf, bool wizard, 
   e.target = (int8_t)target;
   e.conf_flags = (uint8_t)(conf | (wizard ? 0x10 : 0));
   e.len = (uint8_t)n;
+#if CIT_WAVE
+  if (n <= 64) {
+    int f = g.kh_fill, l = cit_lane();
+    int v = 0;
+    if (l < n) v = (int)card_at(l);
+    if (l < n) g.kh_pool[f + l] = (uint8_t)v;
+    g.kh_fill = (uint8_t)(f + n);
+    return;
+  }
+#endif
   for (int i = 0; i < n; i++) g.kh_pool[g.kh_fill + i] = (uint8_t)card_at(i);
   g.kh_fill = (uint8_t)(g.kh_fill + n);
 }
 // get_a_card_like_it on one entry's hand
 CIT_HD void kh_take_like(CitGame& g, int e, int c) {
+#if CIT_WAVE
+  {
+    int l = cit_lane();
+    int len_l = g.kh[l < CIT_KH_MAX ? l : 0].len;
+    int off = (int)__ockl_wfred_add_u32(l < e && l < CIT_KH_MAX ? (unsigned)len_l : 0u);
+    int n = cit_readlane(len_l, e < CIT_KH_MAX ? e : 0), fill = g.kh_fill, t = card_type(c);
+    if (e >= CIT_KH_MAX || n > 64) goto serial;
+    {
+      int v = g.kh_pool[off + (l < n ? l : 0)];
+      uint64_t m = cit_ballot(l < n && card_type(v) == t);
+      if (!m) return;
+      int s0 = off + __ffsll((unsigned long long)m);     // first byte after the match
+      int cnt = fill - s0;
+      int w[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) w[k] = l + 64 * k < cnt ? g.kh_pool[s0 + l + 64 * k] : 0;
+      __asm__ volatile("" ::: "memory");   // every byte loaded before any is moved
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (l + 64 * k < cnt) g.kh_pool[s0 - 1 + l + 64 * k] = (uint8_t)w[k];
+      g.kh[e].len = (uint8_t)(n - 1);
+      g.kh_fill = (uint8_t)(fill - 1);
+      return;
+    }
+  }
+serial:
+#endif
   int off = kh_off(g, e), n = g.kh[e].len, t = card_type(c);
   for (int i = 0; i < n; i++) {
     if (card_type(g.kh_pool[off + i]) == t) {
@@ -500,13 +574,16 @@ CIT_HD int check_game_ending(CitGame& g) {
 }
 // is_last_round (game.py:173-181)
 CIT_HD void is_last_round(CitGame& g) {
-  if (g.ending) return;
 #if CIT_WAVE
   {
+    // both loads issued before either is tested: one LDS round trip
     int i = cit_lane();
-    if (!cit_ballot(i < CIT_NP && g.pl[i < CIT_NP ? i : 0].n_build == 7)) return;
+    int ending = g.ending;
+    int nb = g.pl[i < CIT_NP ? i : 0].n_build;
+    if (ending || !cit_ballot(i < CIT_NP && nb == 7)) return;
   }
 #endif
+  if (g.ending) return;
   for (int i = 0; i < CIT_NP; i++)
     if (g.pl[i].n_build == 7) {
       g.ending = 1;
@@ -1249,6 +1326,18 @@ CIT_HD void confirm_roles(CitGame& g, int q) {
 }
 // move_crown + troneroom_owner_gold (option_functions.py:588-595,625-631)
 CIT_HD void move_crown(CitGame& g, int t) {
+#if CIT_WAVE
+  {
+    int l = cit_lane();
+    int f = g.pl[l < CIT_NP ? l : 0].flags;
+    uint64_t cm = cit_ballot(l < CIT_NP && (f & PF_CROWN));
+    if (cm) g.pl[__ffsll((unsigned long long)cm) - 1].flags &= (uint8_t)~PF_CROWN;
+    g.pl[t].flags |= PF_CROWN;
+    int o = seat_with_type(g, 32);
+    if (o >= 0) g.pl[o].gold++;
+    return;
+  }
+#endif
   for (int p = 0; p < CIT_NP; p++)
     if (g.pl[p].flags & PF_CROWN) { g.pl[p].flags &= (uint8_t)~PF_CROWN; break; }
   g.pl[t].flags |= PF_CROWN;
@@ -1298,7 +1387,7 @@ CIT_HD int do_finish(CitGame& g, const CitOpt& o, CitMT& rng) {
   CitPlayer& P = g.pl[a];
   bool dead = rp_of(g, P.role) & RP_DEAD;
   if (g.err) return -1;
-  if (!dead) {
+  if (!dead && P.n_hand == 0) {     // (the reference tests the building first; both tests are pure)
     if (p_has(P, 28) && P.n_hand == 0) draw_into(g, rng, JD(P), 2);
     if (p_has(P, 30) && P.n_hand == 0) P.gold++;
   }
@@ -1390,6 +1479,21 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
     case O_WHICH_CARD: {                                     // :58-66
       put_card(g, HAND(P), take_like(P.jd, P.n_jd, o.a));
       if (o.b != CIT_NO_CARD) put_card(g, HAND(P), take_like(P.jd, P.n_jd, o.b));
+#if CIT_WAVE
+      {
+        int i = cit_lane(), nj = P.n_jd, nd = g.n_deck;
+        if (nj <= 64 && nd + nj <= CIT_DECK_CAP - 1) {   // no overflow: one store by all lanes
+          int c = i < nj ? P.jd[i] : CIT_NO_CARD;
+          bool v = i < nj && c != CIT_NO_CARD;
+          uint64_t m = cit_ballot(v);
+          if (v) deck_ref(g, nd + cit_lane_rank(m)) = (uint8_t)c;
+          g.n_deck = (uint8_t)(nd + __popcll(m));
+          P.n_jd = 0;
+          gs_set(g, 3, a);
+          break;
+        }
+      }
+#endif
       for (int i = 0; i < P.n_jd; i++) deck_put(g, P.jd[i]);
       P.n_jd = 0;
       gs_set(g, 3, a);
@@ -1549,8 +1653,17 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
     case O_TAKE_FROM_HAND: {                                 // :312-328
       CitPlayer& T = g.pl[o.target];
       int e = -1;
+#if CIT_WAVE
+      {
+        int l = cit_lane(), nk = g.n_kh;
+        CitKH k = g.kh[l < CIT_KH_MAX ? l : 0];
+        uint64_t m = cit_ballot(l < nk && l < CIT_KH_MAX && k.owner == a && (k.conf_flags & 0x10));
+        e = m ? __ffsll((unsigned long long)m) - 1 : -1;
+      }
+#else
       for (int i = 0; i < g.n_kh; i++)
         if (g.kh[i].owner == a && (g.kh[i].conf_flags & 0x10)) { e = i; break; }
+#endif
       if (e < 0) { g.err |= CIT_ERR_ATTR; break; }
       put_card(g, HAND(P), take_like(T.hand, T.n_hand, o.a));
       if (o.flags & OF_BUILD) {
@@ -1643,8 +1756,17 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       break;
     case O_ABBOT_BEG: {                                      // :414-420
       int best = 0;
+#if CIT_WAVE
+      {
+        int l = cit_lane();
+        int gl = l < CIT_NP ? g.pl[l].gold : -32768;
+        int mx = __ockl_wfred_max_i32(gl);
+        best = __ffsll((unsigned long long)cit_ballot(l < CIT_NP && gl == mx)) - 1;   // first maximum
+      }
+#else
       for (int p = 1; p < CIT_NP; p++)
         if (g.pl[p].gold > g.pl[best].gold) best = p;
+#endif
       g.pl[best].gold--;
       int ab = holder_checked(g, 4);
       g.pl[ab].gold++;
@@ -1697,9 +1819,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, take_like(T.build, T.n_build, o.a));
       settle(g, O_WARLORD, a, o.target, o.a);
       at5(g, a, ADM_ABILITY);
-      int owner = -1;
-      for (int p = 0; p < CIT_NP; p++)
-        if (p_has(g.pl[p], 24)) { owner = p; break; }
+      int owner = seat_with_type(g, 24);
       if (owner >= 0 && owner != a) {
         gs_set(g, 6, owner);
         g.gs_intr = 1;

@@ -183,7 +183,7 @@ __device__ int prof_step(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* buf, in
 
 // The hot loop (default): one game per workgroup (uniform_game), row and
 // MT19937 words in LDS for the whole rollout.
-__global__ __launch_bounds__(64) void k_rollout_u(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_rollout_u(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
                                                  int max_steps, int32_t* steps_out, int32_t* winner) {
   __shared__ __attribute__((aligned(16))) CitOpt buf[ROLLOUT_BUF ? ROLLOUT_BUF : 1];
   uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {

@@ -81,6 +81,24 @@ struct CfrTree {
 #define CFR_TEAM 1
 #endif
 
+// The search's working state (the CfrTree, the two MT19937 streams, the
+// working rows w0/w1, the determinization scratch) lives in LDS, but the
+// out-of-line functions below receive it through generic references, which
+// the compiler addresses with flat instructions.  cfr_lds() re-derives such a
+// reference through an LDS pointer, so everything inlined below it uses ds_*
+// instructions.  Only for CIT_WAVE units (the search kernels); the
+// one-tree-per-lane target kernels and the host build keep plain references.
+#if CIT_WAVE
+template <class X>
+__device__ __forceinline__ X& cfr_lds(X& x) {
+  __builtin_assume(__builtin_amdgcn_is_shared((const void*)&x));
+  return x;
+}
+#else
+template <class X>
+CIT_HD X& cfr_lds(X& x) { return x; }
+#endif
+
 // One out-of-line copy of each engine entry point for the search: the
 // engine is force-inlined by default (the rollout kernel wants that), and
 // inlining it at every call site of the search multiplies code size and
@@ -112,25 +130,25 @@ struct CitProf {
 #define CIT_PROF_SCOPE(i) ((void)0)
 #endif
 CIT_NOINLINE int eng_carry(CitGame& g, const CitOpt& o, CitMT& r) {
-  CIT_PROF_SCOPE(0); return cit_carry_out(g, o, r); }
+  CIT_PROF_SCOPE(0); return cit_carry_out(cfr_lds(g), o, cfr_lds(r)); }
 CIT_NOINLINE void eng_prepare(CitGame& g, CitMT& r, uint64_t* seer) {
-  CIT_PROF_SCOPE(1); cit_prepare_options(g, r, seer); }
+  CIT_PROF_SCOPE(1); cit_prepare_options(cfr_lds(g), cfr_lds(r), seer); }
 CIT_NOINLINE int eng_count(const CitGame& g, uint32_t& err, const uint64_t* seer) {
   CIT_PROF_SCOPE(2);
-  return cit_count_options(g, err, seer);
+  return cit_count_options(cfr_lds(g), err, seer);
 }
 CIT_NOINLINE CitOpt eng_pick(const CitGame& g, int k, const uint64_t* seer) {
-  CIT_PROF_SCOPE(3); return cit_pick_option(g, k, seer); }
+  CIT_PROF_SCOPE(3); return cit_pick_option(cfr_lds(g), k, seer); }
 CIT_NOINLINE int eng_list(const CitGame& g, CitOpt* buf, int cap, uint32_t& err, const uint64_t* seer) {
   CIT_PROF_SCOPE(4);
   ListSink s(buf, cap);
-  cit_enum_options(g, s, seer);
+  cit_enum_options(cfr_lds(g), s, seer);
   err |= s.err;
   return s.n;
 }
 CIT_NOINLINE void eng_sample(CitGame& g, int orig, bool role_sample, CitMT& r, uint8_t* unk) {
   CIT_PROF_SCOPE(5);
-  cit_sample_private(g, orig, role_sample, r, unk);
+  cit_sample_private(cfr_lds(g), orig, role_sample, cfr_lds(r), &cfr_lds(*unk));
 }
 
 CIT_HD uint32_t* row_of(const CfrTree& T, int id) { return T.rows + (long)id * (CIT_GAME_BYTES / 4); }
@@ -282,14 +300,16 @@ CIT_HD void opt_mutate(CitOpt& o, const CitGame& g) {
 }
 
 // -------------------------------------------------------------- nodes
-CIT_NOINLINE void tree_carry(CfrTree& T, CitGame& g, const CitOpt& o, int& winner) {
+CIT_NOINLINE void tree_carry(CfrTree& T_in, CitGame& g, const CitOpt& o, int& winner) {
+  CfrTree& T = cfr_lds(T_in);
   winner = eng_carry(g, o, T.py);
   T.carry_outs++;
 }
 
 // CFRNode(game=w, parent, depth): skip_false_choice on w, then a new node
 // whose row is w.  Returns the node id (-1 on error).
-CIT_NOINLINE int cfr_node(CfrTree& T, CitGame& w, int parent, int depth) {
+CIT_NOINLINE int cfr_node(CfrTree& T_in, CitGame& w, int parent, int depth) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(7);
   uint32_t e = 0;
   eng_prepare(w, T.py, T.seer);
@@ -337,7 +357,8 @@ CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
 }
 
 // ------------------------------------------------------------ expansion
-CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T, int n) {
+CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(8);            // :102-131
   int f = alloc_edges(T, CFR_ROLE_CHILDREN);
   if (f < 0) return;
@@ -370,7 +391,8 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T, int n) {
   }
 }
 
-CIT_NOINLINE void cfr_expand_own(CfrTree& T, int n) {
+CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(9);                   // :133-151
   CitGame& g = *T.w0;
   copy_row(T, reinterpret_cast<uint32_t*>(&g), row_of(T, n));
@@ -408,7 +430,8 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T, int n) {
   }
 }
 
-CIT_NOINLINE void cfr_expand_opponent(CfrTree& T, int n) {
+CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(10);              // :153-179
   CfrNode& N = T.nodes[n];
   copy_row(T, reinterpret_cast<uint32_t*>(T.w1), row_of(T, n));
@@ -456,7 +479,8 @@ CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
 }
 
 // ---------------------------------------------------------- strategies
-CIT_NOINLINE void cfr_update_strategy(CfrTree& T, int n) {
+CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(11);               // :292-319
   CfrNode& N = T.nodes[n];
   int nch = N.n_children;
@@ -496,7 +520,8 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T, int n) {
 }
 
 // action_choice(live=False) (:67-91): returns the edge index within the node
-CIT_NOINLINE int cfr_choose(CfrTree& T, int n) {
+CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(12);
   CfrNode& N = T.nodes[n];
   int nch = N.n_children;
@@ -522,7 +547,8 @@ CIT_NOINLINE int cfr_choose(CfrTree& T, int n) {
 }
 
 // ------------------------------------------------------------- backup
-CIT_NOINLINE void cfr_update_regrets(CfrTree& T, int n) {
+CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(13);                // :231-256
   CfrNode& N = T.nodes[n];
   CfrEdge* E = T.edges + N.first_edge;
@@ -545,7 +571,8 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T, int n) {
   }
 }
 
-CIT_NOINLINE void cfr_backprop(CfrTree& T, int n, const double* reward, bool model) {
+CIT_NOINLINE void cfr_backprop(CfrTree& T_in, int n, const double* reward, bool model) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(14);   // :276-290
   while (n >= 0) {
     CfrNode& N = T.nodes[n];
@@ -591,7 +618,8 @@ CIT_HD int cfr_train(CfrTree& T, int iters) {
 }
 
 // action_choice(live=True) at the root (:67-91; game.py:312-317 for a role pick).
-CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T, int root) {
+CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
+  CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(15);
   CfrNode& N = T.nodes[root];
   if (!(N.flags & NF_ROLE_PICK)) {
@@ -646,7 +674,8 @@ CIT_HD void cfr_state_save(const CfrTree& T, CfrState& S) {
   S.carry_outs = (int32_t)T.carry_outs;
 }
 
-CIT_NOINLINE void cfr_write_feat(CfrTree& T, int n, float* feat) {
+CIT_NOINLINE void cfr_write_feat(CfrTree& T_in, int n, float* feat) {
+  CfrTree& T = cfr_lds(T_in);
   const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
   int pid = (T.nodes[n].flags & NF_ROLE_PICK) ? 5 : -1;
   CFR_SYNC();
@@ -656,8 +685,10 @@ CIT_NOINLINE void cfr_write_feat(CfrTree& T, int n, float* feat) {
 
 // One resumption.  w0 must hold the lane's game when S.phase == CP_INIT.
 // Returns 1 when suspended for an evaluation, 0 when done (S.phase == CP_DONE).
-CIT_NOINLINE int cfr_pred_run(CfrTree& T, CfrState& S, int iters, int max_depth, const float* probs, float* feat,
+CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_depth, const float* probs, float* feat,
                               CitOpt& chosen) {
+  CfrTree& T = cfr_lds(T_in);
+  CfrState& S = cfr_lds(S_in);
   if (S.phase == CP_DONE) return 0;
   if (S.phase == CP_INIT) {
     S.orig = T.orig;

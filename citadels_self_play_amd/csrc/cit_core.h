@@ -374,6 +374,7 @@ CIT_HD uint32_t mt_next(CitMT& r) {
     }
     return (uint32_t)__builtin_amdgcn_readlane((int)r.win, (int)(i & 63u));
   }
+  if (r.coop) return mt_temper(((const cit_lds_u32*)r.mt)[i]);   // coop streams live in LDS (stride 1)
 #endif
   return mt_temper(mt_word(r, (int)i));
 }

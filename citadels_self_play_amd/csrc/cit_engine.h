@@ -957,6 +957,21 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
       if (g.n_deck) EMIT(mk(O_SCHOLAR, a));
       return false;
     case R_WARLORD:
+#if CIT_WAVE
+      {
+        // all seats at once: lane l = building l % 10 of seat l / 10 (p-major
+        // order, as the loops); `seen` is per seat, so the key carries the seat
+        int l = cit_lane(), p = l / 10, i = l - 10 * p, ps = p < CIT_NP ? p : 0;
+        int nb = g.pl[ps].n_build, role = g.pl[ps].role, gold = P.gold;
+        int b = g.pl[ps].build[i];
+        if (!cit_ballot(i == 0 && p < CIT_NP && nb > 10)) {
+          int t = card_type(b);
+          bool q = p < CIT_NP && i < nb && nb < 7 && role != R_BISHOP && card_cost(b) - 1 <= gold && t != 17;
+          WEMIT(cit_first_key(q, p * 64 + t), mk(O_WARLORD, a, p, b));
+          return false;
+        }
+      }
+#endif
       for (int p = 0; p < CIT_NP; p++) {
         const CitPlayer& Q = g.pl[p];
         if (Q.n_build >= 7 || Q.role == R_BISHOP) continue;

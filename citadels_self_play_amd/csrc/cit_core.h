@@ -13,6 +13,7 @@
 //   CitPlayer::kr        RoleKnowlage           game/helper_classes.py:45-70
 //   CitMT                CPython `random` / numpy RandomState (MT19937)
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)

@@ -83,7 +83,7 @@ def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None):
     return b, chosen, stats, rounds
 
 
-def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None):
+def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_cap=None):
     """simulate_game (train_from_scratch.py:23-36, pretrain / training=True: the
     search ignores the model) for every seed: random.seed(s), np.random.seed(s),
     create_a_random_game(max_move), run_mccfr(iters, training=True),
@@ -92,7 +92,7 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None):
     b.random_position(max_move)
     b.seed_numpy()
     cap = node_cap or max(1024, 4 * iters)
-    chosen, stats = b.cfr_decide(iters, node_cap=cap)
+    chosen, stats = b.cfr_decide(iters, node_cap=cap, edge_cap=edge_cap)
     targets = b.cfr_targets(stats[:, 0], mode=0)
     return b, stats, targets
 

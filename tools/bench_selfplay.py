@@ -36,11 +36,15 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per GPU")
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--node-cap", type=int, default=None)
+    ap.add_argument("--edge-cap", type=int, default=None, help="default 8 x node cap (config 5: 2.5 x)")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--seed", type=int, default=30_000_000)
     a = ap.parse_args()
     rank, world, dev = selfplay.init_distributed()
-    B = a.batch or {3: 1024, 4: 4096 // max(1, world) if world > 1 else 4096, 5: 256}[a.config]
+    # config 5: 1024 trees per GPU (one wave per SIMD); a 20000-step tree peaks at
+    # ~83 k nodes / 190 k edges, so the default pool (5 x iters nodes, 2.5 x as
+    # many edges: 219 GB per GPU at 1024 trees) avoids overflow re-searches
+    B = a.batch or {3: 1024, 4: 4096 // max(1, world) if world > 1 else 4096, 5: 1024}[a.config]
     iters = a.iters or {3: 200, 4: 200, 5: 20000}[a.config]
     net = None
     if a.config == 4:
@@ -67,7 +71,8 @@ def main():
         elif a.config == 4:
             chosen, stats, rounds = b.cfr_pred(iters, net, max_depth=10, node_cap=a.node_cap or 2048)
         else:
-            b, stats, t = selfplay.simulate_games(seeds, iters, node_cap=a.node_cap)
+            nc = a.node_cap or max(1024, 5 * iters)
+            b, stats, t = selfplay.simulate_games(seeds, iters, node_cap=nc, edge_cap=a.edge_cap or 5 * nc // 2)
             f, v = selfplay.all_gather_targets(t["feat"], t["value"])
             n_targets = int(f.shape[0])
             term = b.terminal()            # k = 1 picks the final (terminal) game: ValueError in the reference
@@ -77,17 +82,18 @@ def main():
         el = time.perf_counter() - t0
         st = stats.to(dev).to(torch.float64)
         tot = torch.tensor([el, float(b.B), float(st[:, 3].sum()), float(((st[:, 4] != 0) & ~term).sum()),
-                            float(term.sum()), float(st[:, 1].sum()), float(st[:, 1].max())], dtype=torch.float64,
+                            float(term.sum()), float(st[:, 1].sum()), float(st[:, 1].max()), float(st[:, 2].max())],
+                           dtype=torch.float64,
                            device=dev)
         if world > 1:
             tmax = tot.clone()
             dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
             dist.all_reduce(tot)
-            tot[0], tot[6] = tmax[0], tmax[6]
-        el, units, carry, errs, terms, nodes, nodes_max = [float(x) for x in tot]
+            tot[0], tot[6], tot[7] = tmax[0], tmax[6], tmax[7]
+        el, units, carry, errs, terms, nodes, nodes_max, edges_max = [float(x) for x in tot]
         out.append({"config": a.config, "n_gpus": world, "per_gpu": B, "iters": iters, "seconds": el,
                     ("trees_per_s" if a.config == 5 else "decisions_per_s"): units / el,
-                    "carry_out_per_s": carry / el, "nodes_mean": nodes / units, "nodes_max": int(nodes_max), "rounds": rounds,
+                    "carry_out_per_s": carry / el, "nodes_mean": nodes / units, "nodes_max": int(nodes_max), "edges_max": int(edges_max), "rounds": rounds,
                     "pooled_targets": n_targets, "error_lanes_nonterminal": int(errs),
                     "terminal_positions": int(terms)})
     if rank == 0:

@@ -27,6 +27,7 @@
 #define CFR_OPP_CHILDREN 10
 #define CFR_ROLE_CHILDREN 10
 #define CFR_OPT_CAP 512
+#define CFR_LBUF 32                      // options listed into LDS per search step
 #define CFR_LN13 0x1.0ca937be1b9dcp-2   // np.log(1.3)
 #define CFR_ATOL 1.4901161193847656e-08  // sqrt(finfo(float64).eps), numpy choice's p check
 
@@ -64,6 +65,7 @@ struct CfrTree {
   CitGame* w0;                         // working rows (LDS on the device)
   CitGame* w1;
   uint8_t* tmp;                        // >= CIT_USED_CAP bytes scratch
+  CitOpt* lbuf;                        // CFR_LBUF descriptors (LDS on the device)
   uint32_t err;
   uint32_t carry_outs;
 };
@@ -142,6 +144,16 @@ CIT_NOINLINE CitOpt eng_pick(const CitGame& g, int k, const uint64_t* seer) {
 CIT_NOINLINE int eng_list(const CitGame& g, CitOpt* buf, int cap, uint32_t& err, const uint64_t* seer) {
   CIT_PROF_SCOPE(4);
   ListSink s(buf, cap);
+  cit_enum_options(cfr_lds(g), s, seer);
+  err |= s.err;
+  return s.n;
+}
+// A search step's option list: the first CFR_LBUF options land in T.lbuf (LDS)
+// while all are counted, so one enumeration serves both the count and the
+// draw (opt_at re-enumerates only for an index past the buffer).
+CIT_NOINLINE int eng_list_lds(const CitGame& g, CitOpt* lbuf, uint32_t& err, const uint64_t* seer) {
+  CIT_PROF_SCOPE(2);
+  ListSink s(&cfr_lds(*lbuf), CFR_LBUF);
   cit_enum_options(cfr_lds(g), s, seer);
   err |= s.err;
   return s.n;
@@ -313,17 +325,17 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, CitGame& w, int parent, int depth) {
   CIT_PROF_SCOPE(7);
   uint32_t e = 0;
   eng_prepare(w, T.py, T.seer);
-  int n = eng_count(w, e, T.seer);
+  int n = eng_list_lds(w, T.lbuf, e, T.seer);
   int i = 0;
   bool done = false;
   while (n == 1 && !done && !e && !w.err) {
     i++;
-    CitOpt o = eng_pick(w, 0, T.seer);
+    CitOpt o = T.lbuf[0];
     int win;
     tree_carry(T, w, o, win);
     done = win >= 0;
     eng_prepare(w, T.py, T.seer);
-    n = eng_count(w, e, T.seer);
+    n = eng_list_lds(w, T.lbuf, e, T.seer);
     if (i > 100) done = true;
   }
   T.err |= e | w.err;
@@ -373,11 +385,11 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
     while (h.gs_state != 1 && !T.err) {
       uint32_t e = 0;
       eng_prepare(h, T.py, T.seer);
-      int cnt = eng_count(h, e, T.seer);
+      int cnt = eng_list_lds(h, T.lbuf, e, T.seer);
       T.err |= e;
       int k = np_choice_uniform(T.np, cnt, T.err);
       if (T.err) break;
-      last = eng_pick(h, k, T.seer);
+      last = k < CFR_LBUF ? T.lbuf[k] : eng_pick(h, k, T.seer);
       int win;
       tree_carry(T, h, last, win);
       T.err |= h.err;
@@ -441,11 +453,11 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
     eng_sample(h, T.orig, par >= 0 && T.nodes[par].gs_state != 0, T.py, T.tmp);
   uint32_t e = 0;
   eng_prepare(h, T.py, T.seer);
-  int cnt = eng_count(h, e, T.seer);
+  int cnt = eng_list_lds(h, T.lbuf, e, T.seer);
   T.err |= e | h.err;
   int k = np_choice_uniform(T.np, cnt, T.err);
   if (T.err) return;
-  CitOpt o = eng_pick(h, k, T.seer);
+  CitOpt o = k < CFR_LBUF ? T.lbuf[k] : eng_pick(h, k, T.seer);
   opt_mutate(o, h);
   CitOpt key = opt_key(o, h);
   int win;

@@ -36,6 +36,7 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   __shared__ __attribute__((aligned(16))) uint32_t w0s[ROW_W];
   __shared__ __attribute__((aligned(16))) uint32_t w1s[ROW_W];
   __shared__ __attribute__((aligned(16))) uint8_t tmps[128];
+  __shared__ __attribute__((aligned(16))) CitOpt lbufs[CFR_LBUF];
   long l = blockIdx.x;
   if (l >= B) return;
   long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
@@ -56,6 +57,7 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   T.w0 = reinterpret_cast<CitGame*>(w0s);
   T.w1 = reinterpret_cast<CitGame*>(w1s);
   T.tmp = tmps;
+  T.lbuf = lbufs;
   T.err = 0;
   T.carry_outs = 0;
   copy_row(T, w0s, games + l * ROW_W);
@@ -88,6 +90,7 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   __shared__ __attribute__((aligned(16))) uint32_t w0s[ROW_W];
   __shared__ __attribute__((aligned(16))) uint32_t w1s[ROW_W];
   __shared__ __attribute__((aligned(16))) uint8_t tmps[128];
+  __shared__ __attribute__((aligned(16))) CitOpt lbufs[CFR_LBUF];
   long l = blockIdx.x;
   if (l >= B) return;
   __shared__ CfrState S;
@@ -110,6 +113,7 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   T.w0 = reinterpret_cast<CitGame*>(w0s);
   T.w1 = reinterpret_cast<CitGame*>(w1s);
   T.tmp = tmps;
+  T.lbuf = lbufs;
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;

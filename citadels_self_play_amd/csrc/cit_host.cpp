@@ -153,6 +153,7 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
   CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   uint8_t tmp[128];
+  CitOpt lbuf[CFR_LBUF];
   for (int l = 0; l < B; l++) {
     uint8_t* base = pool + per * l;
     CfrTree T;
@@ -171,6 +172,7 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
     T.w0 = w0;
     T.w1 = w1;
     T.tmp = tmp;
+    T.lbuf = lbuf;
     T.err = 0;
     T.carry_outs = 0;
     memcpy(w0, &g[l], CIT_GAME_BYTES);
@@ -207,6 +209,7 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
   CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   uint8_t tmp[128];
+  CitOpt lbuf[CFR_LBUF];
   int waiting = 0;
   for (int l = 0; l < B; l++) {
     CfrState& S = st[l];
@@ -226,6 +229,7 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
     T.w0 = w0;
     T.w1 = w1;
     T.tmp = tmp;
+    T.lbuf = lbuf;
     if (S.phase == CP_INIT) {
       T.n_nodes = T.n_edges = 0;
       T.err = 0;

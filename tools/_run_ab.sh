@@ -6,4 +6,4 @@ for v in "$@"; do
 done &&
 timeout -k 10 200 python tools/bench_selfplay.py --config 3 > gpurun_out/cfg3.log 2>&1 &&
 timeout -k 10 200 python tools/bench_selfplay.py --config 4 > gpurun_out/cfg4.log 2>&1 &&
-timeout -k 10 200 python tools/bench_selfplay.py --config 5 > gpurun_out/cfg5.log 2>&1
+timeout -k 10 300 python tools/bench_selfplay.py --config 5 --reps 1 > gpurun_out/cfg5.log 2>&1

@@ -84,15 +84,18 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, the real path); gloo only to rehearse N>1 ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; modulo only matters when rehearsing N ranks on fewer GPUs
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        dist.init_process_group(args.dist_backend)
     torch.cuda.set_device(dev)
 
     from citadels_self_play_amd import layout as L

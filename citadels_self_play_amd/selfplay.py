@@ -34,14 +34,21 @@ TARGET_ROW_BYTES = 418 * 4 + 6 * 8      # encode_game f32[418] | node_value f64[
 
 def init_distributed():
     """One process per GPU under torchrun (RANK / LOCAL_RANK / WORLD_SIZE); RCCL
-    ("nccl") process group when WORLD_SIZE > 1.  Returns (rank, world, device)."""
+    ("nccl") process group when WORLD_SIZE > 1.  Returns (rank, world, device).
+    CIT_DIST_BACKEND=gloo (with ranks folded onto the visible GPUs) exists only
+    to rehearse N ranks on a one-GPU box; the product path is RCCL."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if ws > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("CIT_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     r, w = world()
-    return r, w, torch.device("cuda", local)
+    return r, w, dev
 
 
 def world():

@@ -12,7 +12,7 @@ import __graft_entry__ as G  # noqa: E402
 
 
 def build(name, extra):
-    out = os.path.join(ROOT, "build", "ab")
+    out = os.path.join(ROOT, "build", os.environ.get("ABDIR", "ab"))
     os.makedirs(out, exist_ok=True)
     o = os.path.join(out, name + ".o")
     flags = [f for f in G.HIP_FLAGS if not (f.startswith("-O") and any(e.startswith("-O") for e in extra))]

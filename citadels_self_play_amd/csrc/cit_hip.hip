@@ -18,7 +18,7 @@ static_assert(sizeof(CitOpt) == sizeof(CitOption), "descriptor layouts differ");
 
 #define ROW_W (CIT_GAME_BYTES / 4)
 #ifndef ROLLOUT_BUF
-#define ROLLOUT_BUF 32
+#define ROLLOUT_BUF 64   // options listed per step; 64 measured 1.3-1.5 % over 32 (preset max 56)
 #endif
 
 namespace {

@@ -27,7 +27,10 @@
 #define CFR_OPP_CHILDREN 10
 #define CFR_ROLE_CHILDREN 10
 #define CFR_OPT_CAP 512
-#define CFR_LBUF 32                      // options listed into LDS per search step
+#ifndef CFR_LBUF
+#define CFR_LBUF 32
+#endif
+// options listed into LDS per search step
 #define CFR_LN13 0x1.0ca937be1b9dcp-2   // np.log(1.3)
 #define CFR_ATOL 1.4901161193847656e-08  // sqrt(finfo(float64).eps), numpy choice's p check
 

@@ -5,10 +5,16 @@ Checks, in order of strength:
   * every golden trajectory step by step through the per-step ABI
     (cit_get_options -> cit_random_choice -> cit_carry_out): option-list
     digest, chosen index, post-state digest, full states — bit-exact;
-  * the fused rollout kernel reproduces the golden final states;
+  * the fused rollout kernels reproduce the golden final states -- the
+    benchmarked one-game-per-workgroup kernel k_rollout_u
+    (games_per_block=0) and the one-game-per-lane kernel (cit_lanes.hip);
   * fresh seeds against the CPU oracle;
-  * size-independent properties at the benchmark size (B = 4096):
-    determinism, chunked == fused, independence of the workgroup shape.
+  * size-independent properties at the benchmark size (B = 4096, k_rollout_u):
+    determinism, chunked == fused, k_rollout_u == the lanes kernel, lanes vs
+    the oracle;
+  * random-role games at B = 1024 through k_rollout_u, whose option lists
+    exceed its 64-entry LDS buffer (the cit_pick_option path), every lane vs
+    the oracle.
 """
 import numpy as np
 import pytest
@@ -100,7 +106,7 @@ def test_gpu_stepwise_random_role(engine, golden_random):
 @pytest.mark.parametrize("preset", [True, False])
 def test_gpu_rollout_golden(engine, golden_preset, golden_random, preset):
     recs = golden_preset if preset else golden_random
-    for gpb in (1, 16, 64):
+    for gpb in (0, 1, 16, 64):     # 0 = k_rollout_u, the benchmarked kernel
         b = engine([r["seed"] for r in recs], preset=preset)
         steps, w = b.rollout(games_per_block=gpb)
         steps, w = steps.cpu().numpy(), w.cpu().numpy()
@@ -127,32 +133,68 @@ def test_gpu_rollout_vs_oracle_fresh_seeds(engine):
 
 
 def test_gpu_full_size_properties(engine):
-    """B = 4096 (the benchmark configuration): no lane errors, every game ends,
-    chunked stepping == fused rollout == other workgroup shapes, deterministic,
-    and a sample of lanes equals the oracle."""
+    """B = 4096 (the benchmark configuration) through k_rollout_u
+    (games_per_block=0, the kernel bench.py times): no lane errors, every game
+    ends, fused == chunked stepping (k_rollout_u and the lanes kernel) == the
+    one-game-per-lane kernel at two shapes, and 256 lanes equal the oracle."""
     import citadels_oracle as O
     B = 4096
     seeds = np.arange(7_000_000, 7_000_000 + B)
     a = engine(seeds, preset=True)
-    steps_a, w_a = a.rollout(games_per_block=16)
+    steps_a, w_a = a.rollout(games_per_block=0)
     torch.cuda.synchronize()
     assert int((a.errors() != 0).sum()) == 0
     assert bool(a.terminal().all())
     sa = steps_a.cpu().numpy()
+    wa = w_a.cpu().numpy()
     assert sa.min() > 100 and sa.max() < 2000
     rows_a = a.rows()
-    b = engine(seeds, preset=True)
-    while True:
-        b.rollout(max_steps=37, games_per_block=64)
-        if bool(b.terminal().all()) or int((b.errors() != 0).sum()):
-            break
-    assert np.array_equal(b.rows(), rows_a)
-    assert np.array_equal(b.steps.cpu().numpy(), sa)
-    c = engine(seeds, preset=True)
-    c.rollout(games_per_block=4)
-    assert np.array_equal(c.rows(), rows_a)
+    for chunk_gpb in (0, 64):
+        b = engine(seeds, preset=True)
+        while True:
+            b.rollout(max_steps=37, games_per_block=chunk_gpb)
+            if bool(b.terminal().all()) or int((b.errors() != 0).sum()):
+                break
+        assert np.array_equal(b.rows(), rows_a), chunk_gpb
+        assert np.array_equal(b.steps.cpu().numpy(), sa), chunk_gpb
+    for gpb in (4, 16):
+        c = engine(seeds, preset=True)
+        sc, wc = c.rollout(games_per_block=gpb)
+        assert np.array_equal(c.rows(), rows_a), gpb
+        assert np.array_equal(sc.cpu().numpy(), sa) and np.array_equal(wc.cpu().numpy(), wa), gpb
     rng = np.random.default_rng(0)
-    for l in rng.choice(B, 12, replace=False):
+    for l in rng.choice(B, 256, replace=False):
         og, n = O.random_rollout(int(seeds[l]), True)
-        assert sa[l] == n
-        assert canon.canon_game(L.game_from_bytes(rows_a[l])) == O.canon(og)
+        assert sa[l] == n, l
+        assert wa[l] == og.winner, l
+        assert canon.canon_game(L.game_from_bytes(rows_a[l])) == O.canon(og), l
+
+
+def test_gpu_rollout_u_option_overflow(engine):
+    """Random-role games (thousands of options per step for the cardinal /
+    magician) through k_rollout_u at B = 1024: a draw k >= 64 misses the LDS
+    option buffer and takes cit_pick_option (re-enumeration to the k-th
+    option).  Every lane equals the oracle and the lanes kernel; the test
+    asserts the overflow path was actually taken many times."""
+    import citadels_oracle as O
+    B = 1024
+    seeds = np.arange(9_100_000, 9_100_000 + B)
+    a = engine(seeds, preset=False)
+    steps_a, w_a = a.rollout(games_per_block=0)
+    sa, wa = steps_a.cpu().numpy(), w_a.cpu().numpy()
+    assert int((a.errors() != 0).sum()) == 0
+    assert bool(a.terminal().all())
+    rows_a = a.rows()
+    c = engine(seeds, preset=False)
+    sc, wc = c.rollout(games_per_block=8)
+    assert np.array_equal(c.rows(), rows_a)
+    assert np.array_equal(sc.cpu().numpy(), sa) and np.array_equal(wc.cpu().numpy(), wa)
+    big_draws = 0
+    for l, s in enumerate(seeds):
+        trace = []
+        og, n = O.random_rollout(int(s), False, trace=trace)
+        big_draws += sum(1 for t in trace if t[3] >= 64)
+        assert sa[l] == n, l
+        assert wa[l] == og.winner, l
+        assert canon.canon_game(L.game_from_bytes(rows_a[l])) == O.canon(og), l
+    assert big_draws >= 50, big_draws

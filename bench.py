@@ -2,23 +2,46 @@
 
 Workload (BASELINE.json configs[1], "config 2"): per GPU, 4096 preset
 6-player games (run_utils.create_game) played by the uniform random policy
-to terminal.  One bench step = one launch of the fused rollout kernel over a
-fresh batch of 4096 games already resident in HBM (initialised, untimed,
-before the timed region); seeds are disjoint across steps and ranks
-(seed = base + (step * world + rank) * B + lane), so N GPUs play N x 4096
-independent games per step (weak scaling, no data-path collective).
+to terminal.  One bench step = one launch of the fused rollout kernel
+(k_rollout_u) over a fresh batch of 4096 games already resident in HBM
+(initialised, untimed, before the timed region); seeds are disjoint across
+steps and ranks (seed = base + (step * world + rank) * B + lane), so N GPUs
+play N x 4096 independent games per step (weak scaling, no data-path
+collective).
 
 Prints ONE JSON line on rank 0.  `value` = carry_out transitions of all ranks
-/ max-over-ranks wall time of the K timed steps.  `roofline` prices the
-rollout kernel by its algorithmic bytes (2 x CIT_GAME_BYTES per transition,
-SURVEY §8(d)) over its HIP-event duration; `cpu_baseline` times the CPU
-oracle (oracle/citadels_oracle.py) on a bounded sample on rank 0 at N=1.
+/ max-over-ranks wall time of the K timed steps.
+
+* `roofline` prices k_rollout_u by its algorithmic bytes (2 x CIT_GAME_BYTES
+  per transition) over its HIP-event duration against HBM
+  peak; `traffic` is the HBM bytes per launch measured IN THIS RUN by two
+  rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child run of
+  this script (N = 1 only; gfx950 FETCH_SIZE half-count corrected).  Since
+  the kernel keeps each game in LDS, those bytes are far below the
+  algorithmic ones: `roofline.issue` reports what does bound it, from a third
+  --pmc pass of SQ counters: SALU / VALU / LDS instructions per transition,
+  the scalar-issue floor (1 SALU per clock per CU) and the wait fraction.
+* `cpu_baseline` times the build's C++ CPU restatement (the same engine
+  headers compiled with g++, build/libcitadels_hostcheck.so) on 1 host core
+  and on all the cores this process may use, on rank 0 at N = 1, with nproc
+  and the lscpu model; the pure-Python oracle (oracle/) is a secondary
+  figure and the reference's own Python is quoted from BASELINE.md (measured
+  in the survey container; it cannot travel to the GPU box).
+* `e2e` adds the untimed init: games/s with k_init (seeding + deal) inside
+  the timed region.
 """
 import argparse
+import ctypes as C
+import glob
+import csv
 import json
 import multiprocessing as mp
 import os
+import platform
+import signal
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -29,7 +52,14 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+N_CU, CLOCK_HZ, SIMD_PER_CU = 256, 2.4e9, 4
 BASE_SEED = 1_000_000_000
+KERNEL = "k_rollout_u"
+# The reference's own Python, BASELINE.md §2 config 1 (survey container, 8-core Xeon).
+REF_PY = {"1_core": 12301, "8_procs": 83869, "unit": "carry_out transitions/s",
+          "where": "survey container (BASELINE.md), not this box"}
+SQ_SET = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+          "SQ_BUSY_CYCLES", "SQ_INSTS_SMEM"]
 
 
 def _oracle_worker(args):
@@ -50,28 +80,130 @@ def _oracle_worker(args):
     return steps, games, time.perf_counter() - t0
 
 
-def cpu_baseline(procs, budget_s):
+def host_threads():
+    """Cores this process may use: the affinity set, capped by OMP_NUM_THREADS
+    (the GPU box's CPU share is 16 of a much larger machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(seconds, py_seconds):
+    """the build's C++ CPU restatement on 1 core and on all usable
+    cores, plus the Python oracle (secondary)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import hostcheck
+    lib = hostcheck.lib()
+    lib.cith_rollout_timed.argtypes = [C.c_int, C.c_uint64, C.c_double, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.cith_rollout_timed.restype = C.c_int
+    threads = host_threads()
+    legs = {}
+    for name, th in (("1_core", 1), ("all_cores", threads)):
+        g, st, w = C.c_longlong(), C.c_longlong(), C.c_double()
+        err = lib.cith_rollout_timed(1, C.c_uint64(BASE_SEED + 10**9), C.c_double(seconds), th, C.byref(g),
+                                     C.byref(st), C.byref(w))
+        legs[name] = {"value": st.value / w.value, "threads": th, "games": g.value, "transitions": st.value,
+                      "wall_s": w.value, "lane_errors": err}
     ctx = mp.get_context("spawn")
-    t0 = time.perf_counter()
+    procs = threads
     with ctx.Pool(procs) as pool:
-        res = pool.map(_oracle_worker, [(BASE_SEED + 10**8 + i * 10**6, budget_s) for i in range(procs)])
-    wall = time.perf_counter() - t0
-    steps = sum(r[0] for r in res)
-    games = sum(r[1] for r in res)
-    busy = max(r[2] for r in res)
-    return {"value": steps / busy, "unit": "carry_out transitions/s", "cores": procs, "kind": "port",
-            "sample": "%d preset games, uniform random policy to terminal, CPU oracle (pure Python), "
-                      "%d processes x %.0f s (%.1f s wall incl. startup)" % (games, procs, budget_s, wall)}
+        res = pool.map(_oracle_worker, [(BASE_SEED + 10**8 + i * 10**6, py_seconds) for i in range(procs)])
+    py = {"value": sum(r[0] for r in res) / max(r[2] for r in res), "procs": procs,
+          "games": sum(r[1] for r in res), "kind": "port (pure-Python oracle/citadels_oracle.py)"}
+    a = legs["all_cores"]
+    return {"value": a["value"], "unit": "carry_out transitions/s", "cores": a["threads"], "kind": "port",
+            "impl": "cpp-restatement: the engine headers (csrc/cit_engine.h) built with g++ -O3 for the host, "
+                    "one game per thread",
+            "sample": "%d preset games, uniform random policy to terminal, %d threads x %.0f s (all cores) and "
+                      "%d games on 1 core x %.0f s" % (a["games"], a["threads"], seconds, legs["1_core"]["games"],
+                                                     seconds),
+            "one_core": legs["1_core"]["value"], "legs": legs, "nproc": os.cpu_count(),
+            "usable_cores": threads, "cpu_model": cpu_model(), "python_oracle": py,
+            "reference_python": REF_PY}
 
 
-def pmc_traffic():
-    """HBM bytes per rollout launch from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_rollout_latest.json")
-    if not os.path.exists(path):
+def _rows(pattern):
+    out = []
+    for p in glob.glob(pattern, recursive=True):
+        with open(p) as f:
+            out += list(csv.DictReader(f))
+    return out
+
+
+def _pmc_pass(counters, outdir, timeout_s=150):
+    """One rocprofv3 --pmc pass over a short child run of this script (its own
+    process group, killed on timeout).  Returns {counter: mean per launch of
+    k_rollout_u} or raises."""
+    os.makedirs(outdir, exist_ok=True)
+    cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", outdir, "-o", "run", "--",
+                                              sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2",
+                                              "--warmup", "1", "--no-cpu-baseline", "--no-pmc"]
+    env = dict(os.environ, TMPDIR="/tmp")
+    with open(os.path.join(outdir, "log.txt"), "w") as log:
+        p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+        try:
+            rc = p.wait(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            raise RuntimeError("rocprofv3 --pmc %s timed out" % counters)
+    if rc != 0:
+        raise RuntimeError("rocprofv3 --pmc %s exited %d" % (counters, rc))
+    per = {}
+    for r in _rows(os.path.join(outdir, "**", "*counter_collection.csv")):
+        if KERNEL in r.get("Kernel_Name", ""):
+            per.setdefault(r["Counter_Name"], {}).setdefault(r.get("Dispatch_Id", "0"), 0.0)
+            per[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
+    if not per:
+        raise RuntimeError("no %s rows in the rocprofv3 output" % KERNEL)
+    return {k: sum(v.values()) / len(v) for k, v in per.items()}
+
+
+def pmc_in_run():
+    """Three --pmc passes (FETCH_SIZE, WRITE_SIZE, SQ set), each its own child run."""
+    base = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
+    out = {"source": "in-run rocprofv3 --pmc, 3 passes over `bench.py --steps 2 --warmup 1` children"}
+    try:
+        f = _pmc_pass(["FETCH_SIZE"], os.path.join(base, "fetch"))["FETCH_SIZE"]
+        w = _pmc_pass(["WRITE_SIZE"], os.path.join(base, "write"))["WRITE_SIZE"]
+        out["fetch_size_kib"] = f
+        out["write_size_kib"] = w
+        out["hbm_bytes_per_launch"] = 2 * 1024 * f + 1024 * w
+        out["sq"] = _pmc_pass(SQ_SET, os.path.join(base, "sq"))
+    except Exception as e:  # a missing profiler must not cost the bench line
+        out["error"] = str(e)[:300]
+    return out
+
+
+def issue_roofline(sq, trans_per_launch, kernel_ms):
+    """What bounds k_rollout_u: instruction issue, from the SQ counters (per
+    wave instruction counts; SQ_*_CYCLES in quad-cycles, used only as a ratio)."""
+    if not sq or "SQ_INSTS_SALU" not in sq:
         return None
-    with open(path) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch")
+    salu, valu, lds = sq["SQ_INSTS_SALU"], sq.get("SQ_INSTS_VALU", 0.0), sq.get("SQ_INSTS_LDS", 0.0)
+    salu_floor_ms = salu / (N_CU * CLOCK_HZ) * 1e3                     # 1 scalar issue / clk / CU
+    valu_floor_ms = valu * 4 / (N_CU * SIMD_PER_CU * CLOCK_HZ) * 1e3    # wave64 on SIMD16: 4 clk
+    out = {"bound": "salu-issue", "salu_per_transition": salu / trans_per_launch,
+           "valu_per_transition": valu / trans_per_launch, "lds_per_transition": lds / trans_per_launch,
+           "salu_floor_ms": salu_floor_ms, "valu_floor_ms": valu_floor_ms,
+           "frac": salu_floor_ms / kernel_ms,
+           "model": "floor = SQ_INSTS_SALU / (256 CU x 2.4 GHz x 1 SALU/clk); frac = floor / kernel time"}
+    if sq.get("SQ_WAVE_CYCLES"):
+        out["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0.0) / sq["SQ_WAVE_CYCLES"]
+    return out
 
 
 def main():
@@ -80,10 +212,11 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="games per GPU")
-    ap.add_argument("--games-per-block", type=int, default=0, help="0 = auto (1 game per wavefront at B=4096)")
-    ap.add_argument("--cpu-procs", type=int, default=8)
-    ap.add_argument("--cpu-seconds", type=float, default=3.0)
+    ap.add_argument("--games-per-block", type=int, default=0, help="0 = k_rollout_u (one game per workgroup)")
+    ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per C++ CPU-baseline leg")
+    ap.add_argument("--py-seconds", type=float, default=2.0, help="Python-oracle CPU figure")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 --pmc passes")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the real path); gloo only to rehearse N>1 ranks on one GPU")
     args = ap.parse_args()
@@ -91,8 +224,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one rank per GPU; modulo only matters when rehearsing N ranks on fewer GPUs
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    n_dev = torch.cuda.device_count()          # does not initialise the GPU
+    # One rank per GPU.  More ranks than GPUs is only a rehearsal: the ranks are
+    # folded onto the visible GPUs and the line says so ("folded").
+    folded = world > max(1, n_dev)
+    if folded and args.dist_backend == "nccl":
+        raise SystemExit("bench.py: WORLD_SIZE=%d > %d visible GPUs; RCCL needs one rank per GPU "
+                         "(use --dist-backend gloo to rehearse folded ranks)" % (world, n_dev))
+
+    # The PMC passes run as child processes before this process touches the GPU.
+    pmc = pmc_in_run() if (world == 1 and not args.no_pmc) else None
+
+    dev = torch.device("cuda", local % max(1, n_dev))
     if world > 1:
         torch.cuda.set_device(dev)
         dist.init_process_group(args.dist_backend)
@@ -116,15 +259,17 @@ def main():
         gb.rollout()
     torch.cuda.synchronize()
 
+    # HIP events on the stream the kernel is launched on (torch's current stream)
+    stream = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k, gb in enumerate(batches[W:]):
-        evs[k][0].record()
+        evs[k][0].record(stream)
         gb.rollout()
-        evs[k][1].record()
+        evs[k][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -134,12 +279,32 @@ def main():
     trans_rank = sum(int(gb.steps.sum().item()) for gb in batches[W:])
     errs = sum(int((gb.errors() != 0).sum().item()) for gb in batches[W:])
     unfinished = sum(int((~gb.terminal()).sum().item()) for gb in batches[W:])
-    t = torch.tensor([elapsed, float(trans_rank), float(errs), float(unfinished)], dtype=torch.float64, device=dev)
+
+    # End to end: the same K batches re-initialised (k_init: CPython seeding + deal)
+    # and rolled out, init inside the timed region.
+    ie = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for k, gb in enumerate(batches[W:]):
+        ie[k][0].record(stream)
+        gb.reset()
+        ie[k][1].record(stream)
+        gb.rollout()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed_e2e = time.perf_counter() - t1
+    init_ms = float(np.mean([a.elapsed_time(b) for a, b in ie]))
+
+    t = torch.tensor([elapsed, float(trans_rank), float(errs), float(unfinished), elapsed_e2e],
+                     dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
+        elapsed, elapsed_e2e = float(tmax[0]), float(tmax[4])
     trans_all, errs_all, unfinished_all = float(t[1]), int(t[2]), int(t[3])
 
     if rank == 0:
@@ -147,12 +312,13 @@ def main():
         avg_ms = float(np.mean(kernel_ms))
         alg_bytes = per_launch_trans * 2 * L.GAME_BYTES
         achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic()
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        n_gpus = min(world, max(1, n_dev))
         out = {
             "metric": "Option.carry_out steps/sec (whole node), 6-player batched self-play",
             "value": trans_all / elapsed,
             "unit": "carry_out transitions/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": K,
             "warmup": W,
             "ms_per_step": elapsed / K * 1e3,
@@ -160,8 +326,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: seeded preset games (run_utils.create_game), CPython-MT19937 random policy, "
-                    "bit-exact with the reference per seed",
+            "data": "synthetic: seeded preset games (run_utils.create_game), CPython-MT19937 random policy; "
+                    "k_rollout_u is bit-exact with the reference per seed (tests/test_gpu_parity.py)",
             "config": {"workload": "config2: %d preset 6-player games per GPU, uniform random policy to terminal"
                                    % B, "games_per_gpu": B, "games_per_block": args.games_per_block,
                        "rng": "per-game CPython MT19937 (parity mode)", "parallelism": "dp%d" % world},
@@ -170,12 +336,22 @@ def main():
             "unfinished_lanes": unfinished_all,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout", "kernel_avg_ms": avg_ms,
+                         "kernel": KERNEL if args.games_per_block <= 0 else "k_rollout (lanes)",
+                         "kernel_avg_ms": avg_ms,
                          "alg_bytes_per_launch": alg_bytes,
-                         "alg_bytes_per_transition": 2 * L.GAME_BYTES},
+                         "alg_bytes_per_transition": 2 * L.GAME_BYTES,
+                         "measured_gbs": (traffic / (avg_ms * 1e-3) / 1e9) if traffic else None,
+                         "issue": issue_roofline(pmc.get("sq") if pmc else None, per_launch_trans, avg_ms),
+                         "pmc": pmc},
+            "e2e": {"games_per_s": world * B * K / elapsed_e2e, "transitions_per_s": trans_all / elapsed_e2e,
+                    "init_ms_per_batch": init_ms,
+                    "note": "k_init (CPython init_by_array seeding + preset deal) inside the timed region"},
         }
+        if folded:
+            out["folded"] = True
+            out["ranks"] = world
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_procs, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.py_seconds)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

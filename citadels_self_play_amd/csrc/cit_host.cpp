@@ -1,7 +1,10 @@
-// TEST-ONLY host build of the engine headers (g++, no HIP).  Loaded by the
-// CPU test suite to check the engine logic against the golden fixtures in
-// this (GPU-less) container.  It is NOT part of the product path: the Python
-// package only ever loads libcitadels_hip.so and has no CPU fallback.
+// Host build of the engine headers (g++, no HIP).  Two uses, neither on the
+// product path (the Python package only ever loads libcitadels_hip.so and has
+// no CPU fallback):
+//  * the CPU test suite checks the engine logic against the golden fixtures in
+//    this (GPU-less) container;
+//  * bench.py's cpu_baseline leg times cith_rollout_timed, the C++ CPU
+//    restatement SURVEY.md §8(d) asks for, on 1 and on all host cores.
 //
 // Same argument conventions as the HIP C-ABI in include/citadels.h, minus the
 // stream, with host pointers; names are prefixed cith_.
@@ -9,6 +12,11 @@
 #include <string.h>
 
 #include <stdlib.h>
+
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <vector>
 
 #include "cit_cfr.h"
 
@@ -298,6 +306,57 @@ void cith_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, const in
     cfr_emit_targets(T, r, roots[l], mode, l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
     SAVE(r);
   }
+}
+
+// CPU baseline: `threads` host threads each play preset /
+// random-role games seeded seed0, seed0+1, ... (an atomic counter hands out
+// seeds) with the uniform random policy to terminal -- the step loop of
+// compare_to_random.py:37-39 / run_utils.py:37-41 -- until `seconds` have
+// elapsed.  Returns the finished games, their carry_out transitions and the
+// wall time (the last game of each thread runs to its end).
+int cith_rollout_timed(int preset, uint64_t seed0, double seconds, int threads, long long* out_games,
+                       long long* out_steps, double* out_wall) {
+  if (threads <= 0 || seconds < 0) return -1;
+  std::atomic<uint64_t> next(seed0);
+  std::atomic<long long> games(0), steps(0), errs(0);
+  auto t0 = std::chrono::steady_clock::now();
+  auto deadline = t0 + std::chrono::duration<double>(seconds);
+  auto work = [&]() {
+    CitGame* g = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
+    std::vector<uint32_t> mt(CIT_MT_N);
+    std::vector<uint64_t> seer(CIT_SEER_MAX);
+    long long my_games = 0, my_steps = 0, my_errs = 0;
+    while (std::chrono::steady_clock::now() < deadline) {
+      uint64_t seed = next.fetch_add(1);
+      CitMT r;
+      r.mt = mt.data();
+      r.stride = 1;
+      r.pos = 0;
+      r.coop = 0;
+      mt_seed_cpython(r, seed);
+      cit_init_game(*g, r, preset != 0);
+      int s = 0;
+      while (!g->terminal && !g->err && s < CIT_ROLLOUT_CAP) {
+        cit_random_step(*g, r, seer.data());
+        s++;
+      }
+      my_games++;
+      my_steps += s;
+      my_errs += g->err != 0;
+    }
+    games += my_games;
+    steps += my_steps;
+    errs += my_errs;
+    free(g);
+  };
+  std::vector<std::thread> pool;
+  for (int i = 1; i < threads; i++) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  *out_wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  *out_games = games;
+  *out_steps = steps;
+  return (int)errs.load();
 }
 
 }  // extern "C"

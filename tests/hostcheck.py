@@ -21,7 +21,8 @@ def build(force=False):
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(s) for s in srcs):
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-strict-aliasing", "-shared", "-fPIC", srcs[0], "-o", LIB])
+    subprocess.check_call(["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-strict-aliasing", "-shared", "-fPIC",
+                           "-pthread", srcs[0], "-o", LIB])
     return LIB
 
 

@@ -14,7 +14,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "citadels.h")
 
 _lib = None
 
-vp, i32, u64 = C.c_void_p, C.c_int, C.c_uint64
+vp, i32, i64, u64 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64
 
 _SIGS = {
     "cit_abi_version": ([], i32),
@@ -31,10 +31,13 @@ _SIGS = {
     "cit_encode_games": ([vp, i32, i32, vp, vp], i32),
     "cit_encode_options": ([vp, vp, vp, i32, vp, vp], i32),
     "cit_mlp_forward": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
-    "cit_cfr_pool_bytes": ([i32, i32], i32),
+    "cit_cfr_pool_bytes": ([i32, i32], i64),
+    "cit_count_options": ([vp, vp, vp, vp, i32, vp, vp], i32),
+    "cit_determinize": ([vp, vp, vp, i32, vp, i32, vp], i32),
+    "cit_skip_false_choice": ([vp, vp, vp, vp, i32, vp, vp], i32),
     "cit_cfr_opt_cap": ([], i32),
     "cit_advance_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp], i32),
-    "cit_cfr_decide": ([vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, vp], i32),
+    "cit_cfr_decide": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, vp], i32),
     "cit_cfr_state_bytes": ([], i32),
     "cit_randbelow": ([vp, vp, i32, i32, vp, vp], i32),
     "cit_advance_policy": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
@@ -42,8 +45,10 @@ _SIGS = {
     "cit_cfr_target_count": ([vp, i32, i32, i32, vp, i32, vp, vp], i32),
     "cit_cfr_targets": ([vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "cit_close_rows": ([], i32),
+    "cit_cfr_action_choice": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp], i32),
     "cit_close_position": ([vp, vp, vp, vp, i32, vp, vp, vp], i32),
-    "cit_cfr_pred_step": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp], i32),
+    "cit_cfr_pred_step": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp,
+                           vp], i32),
 }
 
 
@@ -55,7 +60,7 @@ def declared_symbols():
     """Function names declared in include/citadels.h."""
     with open(HEADER) as f:
         txt = f.read()
-    return sorted(set(re.findall(r"\bint\s+(cit_\w+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(?:int|int64_t)\s+(cit_\w+)\s*\(", txt)))
 
 
 def load():

@@ -25,13 +25,13 @@ Errors surface as the reference's exception types (IndexError on an empty
 option list, ValueError from np.random.choice, KeyError, ...), raised from
 the lane's error bits after each call.
 
-Differences, by design:
-* `CFRNode(game, ...)` defers skip_false_choice (deep_mccfr.py:37-49) to the
-  search call; `cfr_train`/`cfr_pred` mutate `game` exactly as the reference's
-  constructor would, before anything can observe it.
-* The search and the live decision run in one launch (what run_mccfr does);
-  `action_choice(live=True)` returns that decision.  `action_choice(live=False)`
-  (the in-search sampler) is internal to the device search.
+Search nodes: `CFRNode(game, ...)` runs skip_false_choice (deep_mccfr.py:
+19-20, 37-49) on `game` in its constructor, as the reference does
+(cit_skip_false_choice); the search then builds its root from that game
+(CIT_CFR_ROOT_SKIPPED).  The search and the live decision run in one launch
+(what run_mccfr does): `action_choice(live=True)` returns that decision;
+`action_choice(live=False)` samples a child from the finished tree with the
+in-search sampler (cit_cfr_action_choice, numpy stream).
 """
 import copy as _copy
 
@@ -217,7 +217,8 @@ class Game:
     def packed(self):
         """The CitGame view of the row (host copy, cached until the next mutation)."""
         if self._view is None:
-            self._view = L.game_from_bytes(self.row[0].cpu().numpy())
+            self._raw = self.row[0].cpu().numpy()
+            self._view = L.game_from_bytes(self._raw)
         return self._view
 
     def _check(self, what):
@@ -287,7 +288,8 @@ class Game:
             return self.get_options_from_state(k)
         g = self.packed()
         host = opts[0, :k].cpu().numpy()
-        return [Option(host[i], g) for i in range(k)]
+        raw = self._raw.copy()             # the options' Cards: slots of this game (encode_option reads them)
+        return [Option(host[i], g, raw) for i in range(k)]
 
     def encode_game(self):
         feat = torch.zeros((1, 418), dtype=torch.float32, device=self.device)
@@ -394,8 +396,9 @@ class Option:
     """game/option.py option: `name`, `attributes`, carry_out, encode_option.
     Holds the 16-byte device descriptor it was enumerated as."""
 
-    def __init__(self, desc, g=None):
+    def __init__(self, desc, g=None, row=None):
         self.desc = np.ascontiguousarray(desc, np.uint8).copy()
+        self._row = row
         o = L.opt_from_bytes(self.desc)
         self.name, self.attributes = _typed_attrs(o, g) if g is not None else (OPTION_NAMES[o.name], {})
 
@@ -418,11 +421,14 @@ class Option:
         wi = int(w.item())
         return game.players[wi] if wi >= 0 else None
 
-    def encode_option(self, game=None):
-        """[1, 131] float32 (option.py:52-115)."""
+    def encode_option(self):
+        """[1, 131] float32 (option.py:52-115).  The descriptor names cards by
+        hand slot, so the option keeps the game row it was enumerated on (the
+        reference's option holds the Card objects themselves)."""
         lib = _lib.load()
-        dev = game.device if game is not None else torch.device("cuda")
-        row = game.row if game is not None else torch.zeros((1, L.GAME_BYTES), dtype=torch.uint8, device=dev)
+        dev = torch.device("cuda")
+        row = torch.zeros((1, L.GAME_BYTES), dtype=torch.uint8, device=dev) if self._row is None else \
+            torch.from_numpy(self._row).to(dev).reshape(1, L.GAME_BYTES)
         d = torch.from_numpy(self.desc).to(dev).reshape(1, 16)
         lane = torch.zeros(1, dtype=torch.int32, device=dev)
         out = torch.zeros((1, 131), dtype=torch.float32, device=dev)
@@ -446,6 +452,18 @@ class CFRNode:
         self.node_cap = node_cap
         self._tree = None
         self._chosen = None
+        self._b = None
+        self._skipped = self.skip_false_choice()       # carry_outs the constructor played
+
+    def skip_false_choice(self):
+        """deep_mccfr.py:37-49 on self.game (mutates it, consumes its stream)."""
+        st = self.game.stream
+        c = torch.zeros(1, dtype=torch.int32, device=st.device)
+        _lib.check(st.lib.cit_skip_false_choice(_ptr(self.game.row), _ptr(st.mt), _ptr(st.idx), _ptr(self.game.seer),
+                                                1, _ptr(c), _cs()), "cit_skip_false_choice")
+        self.game._dirty()
+        self.game._check("skip_false_choice")
+        return int(c.item())
 
     # -- search
     def _batch(self):
@@ -455,17 +473,22 @@ class CFRNode:
 
     def cfr_train(self, max_iterations=100000):
         """cfr_train (deep_mccfr.py:187-205) + the live decision of run_mccfr."""
+        from .engine import CFR_ROOT_SKIPPED, pool_caps
         b = self._batch()
-        chosen, stats = b.cfr_decide(max_iterations, node_cap=self.node_cap or max(1024, 4 * max_iterations))
+        nc, ec = (self.node_cap, None) if self.node_cap else pool_caps(max_iterations)
+        chosen, stats = b.cfr_decide(max_iterations, node_cap=nc, edge_cap=ec, flags=CFR_ROOT_SKIPPED,
+                                     orig=self.original_player_id)
         self._finish(b, chosen, stats)
 
     def cfr_pred(self, max_iterations=2000, max_depth=20):
         """cfr_pred (deep_mccfr.py:207-229) with value-net leaves + the live decision."""
         from .models import ValueNet
         net = self.model if isinstance(self.model, ValueNet) else ValueNet(self.model, self.game.device)
+        from .engine import CFR_ROOT_SKIPPED, pool_caps
         b = self._batch()
-        chosen, stats, _ = b.cfr_pred(max_iterations, net, max_depth=max_depth,
-                                      node_cap=self.node_cap or max(2048, 4 * max_iterations))
+        nc, ec = (self.node_cap, None) if self.node_cap else pool_caps(max_iterations)
+        chosen, stats, _ = b.cfr_pred(max_iterations, net, max_depth=max_depth, node_cap=max(2048, nc), edge_cap=ec,
+                                      flags=CFR_ROOT_SKIPPED, orig=self.original_player_id)
         self._finish(b, chosen, stats)
 
     def _finish(self, b, chosen, stats):
@@ -480,13 +503,18 @@ class CFRNode:
         self._err = err
 
     def action_choice(self, live=False):
-        if not live:
-            raise NotImplementedError("the in-search sampler runs inside the device search")
+        """live=True: run_mccfr's decision, (None, option) for a role pick as
+        the reference returns; live=False: (child node, option) drawn by the
+        in-search sampler from the tree (deep_mccfr.py:67-91)."""
         if self._chosen is None:
-            raise RuntimeError("call cfr_train / cfr_pred first")
+            raise ValueError("a must be non-empty (the node has no children before a search)")
         if self._err:
             raise_for(self._err, "action_choice")
-        return None, Option(self._chosen, self.game.packed())
+        if not live:
+            return self.root.action_choice(live=False)
+        if self.root.role_pick_node:
+            return None, Option(self._chosen, self.game.packed(), self.game._raw.copy())
+        return self.root.child_of(self._chosen), Option(self._chosen, self.game.packed(), self.game._raw.copy())
 
     # -- tree views
     def _load(self):
@@ -509,7 +537,8 @@ class CFRNode:
 
     @property
     def carry_outs(self):
-        return int(self._stats[3])
+        """carry_out calls of the search, the constructor's skip_false_choice included."""
+        return int(self._stats[3]) + self._skipped
 
     @property
     def node_count(self):
@@ -529,6 +558,32 @@ class _NodeView:
     def role_pick_node(self):
         return bool(self._N["flags"] & 1)
 
+    def action_choice(self, live=False):
+        """deep_mccfr.py:67-91 with live=False (the in-search sampler), drawn on
+        the device from the tree's numpy stream: (child node, option)."""
+        if live:
+            raise ValueError("live decisions come from the root (CFRNode.action_choice(live=True))")
+        b = self.owner._b
+        d = b.device
+        node = torch.tensor([self.n], dtype=torch.int32, device=d)
+        edge = torch.zeros(1, dtype=torch.int32, device=d)
+        err = torch.zeros(1, dtype=torch.int32, device=d)
+        _lib.check(b.lib.cit_cfr_action_choice(_ptr(b.pool), 1, b.node_cap, b.edge_cap, _ptr(node), _ptr(b.np_mt),
+                                               _ptr(b.np_idx), _ptr(edge), _ptr(err), _cs()), "cit_cfr_action_choice")
+        e = int(err.item())
+        if e:
+            raise_for(e, "action_choice")
+        a = int(edge.item())
+        opt, child = self.children[a]
+        return child, opt
+
+    def child_of(self, desc):
+        """The child whose edge option equals descriptor `desc` (None if absent)."""
+        for e in self._E:
+            if bytes(e["opt"]) == bytes(np.asarray(desc, np.uint8)):
+                return _NodeView(self.owner, int(e["child"]))
+        return None
+
     @property
     def depth(self):
         return int(self._N["depth"])
@@ -541,22 +596,22 @@ class _NodeView:
     def winning_probabilities(self):
         return np.array(self._N["wp"])
 
-    def _arr(self, f):
-        if self.role_pick_node:
-            return np.array(self._E[f]).T.copy()           # [6, 10]
-        return np.array(self._E[f][:, 0])
+    def _arr(self, k):
+        from .engine import node_arrays
+        nodes, edges, _ = self.owner._load()
+        return node_arrays(nodes, edges, self.n)[k]      # [nch], or [6, 10] for a role pick
 
     @property
     def cumulative_regrets(self):
-        return self._arr("R")
+        return self._arr(0)
 
     @property
     def strategy(self):
-        return self._arr("S")
+        return self._arr(1)
 
     @property
     def cumulative_strategy(self):
-        return self._arr("CS")
+        return self._arr(2)
 
     @property
     def game(self):
@@ -565,7 +620,7 @@ class _NodeView:
     @property
     def children(self):
         g = self.game
-        return [(Option(e["opt"], g), _NodeView(self.owner, int(e["child"]))) for e in self._E]
+        return [(Option(e["opt"], g, self._row), _NodeView(self.owner, int(e["child"]))) for e in self._E]
 
     def get_all_targets(self, usefulness_treshold=15):
         """(deep_mccfr.py:258-274) over this node's subtree: a list of

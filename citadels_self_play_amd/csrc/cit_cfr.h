@@ -45,13 +45,24 @@ struct CfrNode {                       // 168 B
   uint8_t pad[6];
   double nv[6], wp[6], pred[6];
 };
-struct CfrEdge {                       // 168 B; normal nodes use index 0 of R/S/CS
+// An edge = (option, child) and the parent's regret / strategy / cumulative
+// strategy entries for it.  A normal node's arrays are [nch] (one double per
+// edge).  A role-pick node's are [6 players, 10]: it reserves
+// CFR_ROLE_CHILDREN edges followed by CFR_ROLE_CHILDREN CfrWide records
+// (3 edge slots each) holding the per-player columns, so a normal edge stays
+// 48 B (the pool of a cfr_train(200000) tree is ~1M edges).
+struct CfrEdge {                       // 48 B
   CitOpt opt;
   int32_t child, pad;
+  double R, S, CS;
+};
+struct CfrWide {                       // 144 B = 3 edge slots
   double R[6], S[6], CS[6];
 };
 static_assert(sizeof(CfrNode) == 168, "CfrNode layout");
-static_assert(sizeof(CfrEdge) == 168, "CfrEdge layout");
+static_assert(sizeof(CfrEdge) == 48, "CfrEdge layout");
+static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
+#define CFR_ROLE_EDGE_SLOTS (CFR_ROLE_CHILDREN * 4)   // 10 edges + 10 wide records
 
 struct CfrTree {
   CfrNode* nodes;
@@ -72,6 +83,27 @@ struct CfrTree {
   uint32_t err;
   uint32_t carry_outs;
 };
+
+// Node pool of one tree: [node_cap CfrNode][edge_cap CfrEdge][node_cap rows];
+// B trees are B consecutive pools.  Sizes are 64-bit: a cfr_train(200000)
+// tree needs ~0.5-1 GB.
+CIT_HD int64_t cfr_pool_bytes(int node_cap, int edge_cap) {
+  return (int64_t)node_cap * (int64_t)sizeof(CfrNode) + (int64_t)edge_cap * (int64_t)sizeof(CfrEdge) +
+         (int64_t)node_cap * CIT_GAME_BYTES;
+}
+CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, long l, int node_cap, int edge_cap) {
+  uint8_t* base = pool + cfr_pool_bytes(node_cap, edge_cap) * (int64_t)l;
+  T.nodes = reinterpret_cast<CfrNode*>(base);
+  T.edges = reinterpret_cast<CfrEdge*>(base + (int64_t)node_cap * (int64_t)sizeof(CfrNode));
+  T.rows = reinterpret_cast<uint32_t*>(base + (int64_t)node_cap * (int64_t)sizeof(CfrNode) +
+                                       (int64_t)edge_cap * (int64_t)sizeof(CfrEdge));
+  T.node_cap = node_cap;
+  T.edge_cap = edge_cap;
+}
+// the [6]-wide regret / strategy columns of role-pick child a
+CIT_HD CfrWide* cfr_wide(const CfrTree& T, int first_edge) {
+  return reinterpret_cast<CfrWide*>(T.edges + first_edge + CFR_ROLE_CHILDREN);
+}
 
 // The 64 lanes of a tree's workgroup (one wavefront) run the search in
 // lockstep on shared state (the CfrTree itself lives in LDS); row copies are
@@ -322,13 +354,18 @@ CIT_NOINLINE void tree_carry(CfrTree& T_in, CitGame& g, const CitOpt& o, int& wi
 }
 
 // CFRNode(game=w, parent, depth): skip_false_choice on w, then a new node
-// whose row is w.  Returns the node id (-1 on error).
-CIT_NOINLINE int cfr_node(CfrTree& T_in, CitGame& w, int parent, int depth) {
+// whose row is w.  `skipped`: the caller already ran skip_false_choice on w
+// (the facade's CFRNode constructor), so it is not run again.  Returns the
+// node id (-1 on error).
+CIT_NOINLINE int cfr_node(CfrTree& T_in, CitGame& w, int parent, int depth, bool skipped = false) {
   CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(7);
   uint32_t e = 0;
-  eng_prepare(w, T.py, T.seer);
-  int n = eng_list_lds(w, T.lbuf, e, T.seer);
+  int n = 0;
+  if (!skipped) {
+    eng_prepare(w, T.py, T.seer);
+    n = eng_list_lds(w, T.lbuf, e, T.seer);
+  }
   int i = 0;
   bool done = false;
   while (n == 1 && !done && !e && !w.err) {
@@ -368,15 +405,18 @@ CIT_HD int alloc_edges(CfrTree& T, int n) {
 CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
   E.opt = o;
   E.child = child;
-  for (int k = 0; k < 6; k++) E.R[k] = E.S[k] = E.CS[k] = 0.0;
+  E.R = E.S = E.CS = 0.0;
 }
 
 // ------------------------------------------------------------ expansion
 CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
   CfrTree& T = cfr_lds(T_in);
   CIT_PROF_SCOPE(8);            // :102-131
-  int f = alloc_edges(T, CFR_ROLE_CHILDREN);
+  int f = alloc_edges(T, CFR_ROLE_EDGE_SLOTS);
   if (f < 0) return;
+  CfrWide* W = cfr_wide(T, f);
+  for (int r = 0; r < CFR_ROLE_CHILDREN; r++)
+    for (int k = 0; k < 6; k++) W[r].R[k] = W[r].S[k] = W[r].CS[k] = 0.0;
   T.nodes[n].first_edge = f;
   T.nodes[n].edge_cap = CFR_ROLE_CHILDREN;
   int depth = T.nodes[n].depth + 1;
@@ -502,35 +542,36 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
   if (nch == 0) return;
   CfrEdge* E = T.edges + N.first_edge;
   if (!(N.flags & NF_ROLE_PICK)) {
-    for (int a = 0; a < nch; a++) E[a].S[0] = exp((-E[a].R[0]) * CFR_LN13);
-    double tot = np_sum([E](int i) { return E[i].S[0]; }, nch, T.err);
-    for (int a = 0; a < nch; a++) E[a].S[0] = tot > 0 ? E[a].S[0] / tot : 1.0 / nch;
-    for (int a = 0; a < nch; a++) E[a].CS[0] += E[a].S[0];
-    double cs = np_sum([E](int i) { return E[i].CS[0]; }, nch, T.err);
-    for (int a = 0; a < nch; a++) E[a].CS[0] = E[a].CS[0] / cs;
+    for (int a = 0; a < nch; a++) E[a].S = exp((-E[a].R) * CFR_LN13);
+    double tot = np_sum([E](int i) { return E[i].S; }, nch, T.err);
+    for (int a = 0; a < nch; a++) E[a].S = tot > 0 ? E[a].S / tot : 1.0 / nch;
+    for (int a = 0; a < nch; a++) E[a].CS += E[a].S;
+    double cs = np_sum([E](int i) { return E[i].CS; }, nch, T.err);
+    for (int a = 0; a < nch; a++) E[a].CS = E[a].CS / cs;
   } else {
     // role pick: [6 players, nch] arrays; totals along players (axis 0, sequential)
+    CfrWide* W = cfr_wide(T, N.first_edge);
     double tots[CFR_ROLE_CHILDREN];
     bool small = false;
     for (int a = 0; a < nch; a++) {
       double tot = 0.0;
       for (int p = 0; p < 6; p++) {
-        E[a].S[p] = exp((-E[a].R[p]) * CFR_LN13);
-        tot = p ? tot + E[a].S[p] : E[a].S[0];
+        W[a].S[p] = exp((-W[a].R[p]) * CFR_LN13);
+        tot = p ? tot + W[a].S[p] : W[a].S[0];
       }
       tots[a] = tot;
       small |= tot <= 1e-8;
     }
     for (int a = 0; a < nch; a++)
       for (int p = 0; p < 6; p++) {
-        double v = E[a].S[p] / tots[a];
-        E[a].S[p] = small ? (tots[a] > 1e-8 ? v : 1.0 / 6) : v;
+        double v = W[a].S[p] / tots[a];
+        W[a].S[p] = small ? (tots[a] > 1e-8 ? v : 1.0 / 6) : v;
       }
     for (int a = 0; a < nch; a++)
-      for (int p = 0; p < 6; p++) E[a].CS[p] += E[a].S[p];
-    double cs = np_sum([E](int i) { return E[i / 6].CS[i % 6]; }, nch * 6, T.err);
+      for (int p = 0; p < 6; p++) W[a].CS[p] += W[a].S[p];
+    double cs = np_sum([W](int i) { return W[i / 6].CS[i % 6]; }, nch * 6, T.err);
     for (int a = 0; a < nch; a++)
-      for (int p = 0; p < 6; p++) E[a].CS[p] = E[a].CS[p] / cs;
+      for (int p = 0; p < 6; p++) W[a].CS[p] = W[a].CS[p] / cs;
   }
 }
 
@@ -542,9 +583,10 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
   int nch = N.n_children;
   const CfrEdge* E = T.edges + (N.first_edge < 0 ? 0 : N.first_edge);
   if (!(N.flags & NF_ROLE_PICK)) {
-    double tot = np_sum([E](int i) { return E[i].CS[0]; }, nch, T.err);
-    return np_choice(T.np, [E, tot](int i) { return E[i].CS[0] / tot; }, nch, T.err);
+    double tot = np_sum([E](int i) { return E[i].CS; }, nch, T.err);
+    return np_choice(T.np, [E, tot](int i) { return E[i].CS / tot; }, nch, T.err);
   }
+  const CfrWide* W = cfr_wide(T, N.first_edge);
   // weighted_average_strategy (:51-65) over turn_orders_for_roles of the node's game
   const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
   if (nch > CFR_ROLE_CHILDREN) { T.err |= CIT_ERR_OVERFLOW; return -1; }
@@ -553,7 +595,7 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
   for (int i = 0; i < CIT_NP; i++) hs += g.turn[i];
   for (int a = 0; a < nch; a++) {
     double acc = 0.0;
-    for (int i = 0; i < CIT_NP; i++) acc += E[a].CS[g.turn[i]] * (double)(CIT_NP - i);
+    for (int i = 0; i < CIT_NP; i++) acc += W[a].CS[g.turn[i]] * (double)(CIT_NP - i);
     w[a] = acc / (double)hs;
   }
   double s = np_sum([&w](int i) { return w[i < CFR_ROLE_CHILDREN ? i : 0]; }, nch, T.err);
@@ -575,13 +617,14 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
       double v = T.nodes[E[a].child].wp[p];
       if (v > mx) mx = v;
     }
-    for (int a = 0; a < nch; a++) E[a].R[0] += mx - T.nodes[E[a].child].wp[p];
+    for (int a = 0; a < nch; a++) E[a].R += mx - T.nodes[E[a].child].wp[p];
   } else {
+    CfrWide* W = cfr_wide(T, N.first_edge);
     for (int a = 0; a < nch; a++) {
       const double* wp = T.nodes[E[a].child].wp;
       double mx = wp[0];
       for (int p = 1; p < 6; p++) mx = (mx != mx || wp[p] != wp[p]) ? NAN : (wp[p] > mx ? wp[p] : mx);
-      for (int p = 0; p < 6; p++) E[a].R[p] += mx - wp[p];
+      for (int p = 0; p < 6; p++) W[a].R[p] += mx - wp[p];
     }
   }
 }
@@ -607,8 +650,8 @@ CIT_NOINLINE void cfr_backprop(CfrTree& T_in, int n, const double* reward, bool 
 // cfr_train(iters) on the game in T.w0 (the root's game: skip_false_choice
 // mutates it, as the reference mutates the game passed to CFRNode).
 // Returns the root id.
-CIT_HD int cfr_train(CfrTree& T, int iters) {
-  int root = cfr_node(T, *T.w0, -1, 0);
+CIT_HD int cfr_train(CfrTree& T, int iters, bool root_skipped = false) {
+  int root = cfr_node(T, *T.w0, -1, 0, root_skipped);
   if (root < 0 || T.err) return root;
   if (T.nodes[root].flags & NF_TERMINAL) return root;
   cfr_expand(T, root);
@@ -649,10 +692,10 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
   int nl = eng_list(g, T.optbuf, CFR_OPT_CAP, le, T.seer);
   T.err |= le;
   int pid = g.gs_pid;
-  const CfrEdge* E = T.edges + N.first_edge;
+  const CfrWide* W = cfr_wide(T, N.first_edge);
   double sum = 0.0;
-  for (int j = 0; j < nl; j++) sum += E[T.optbuf[j].a].S[pid];
-  int j = np_choice(T.np, [&](int i) { return E[T.optbuf[i].a].S[pid] / sum; }, nl, T.err);
+  for (int j = 0; j < nl; j++) sum += W[T.optbuf[j].a].S[pid];
+  int j = np_choice(T.np, [&](int i) { return W[T.optbuf[i].a].S[pid] / sum; }, nl, T.err);
   copy_row(T, row_of(T, root), reinterpret_cast<const uint32_t*>(&g));
   if (T.err || j < 0) return mk(O_NUM_NAMES, 0);
   return T.optbuf[j];
@@ -701,13 +744,13 @@ CIT_NOINLINE void cfr_write_feat(CfrTree& T_in, int n, float* feat) {
 // One resumption.  w0 must hold the lane's game when S.phase == CP_INIT.
 // Returns 1 when suspended for an evaluation, 0 when done (S.phase == CP_DONE).
 CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_depth, const float* probs, float* feat,
-                              CitOpt& chosen) {
+                              CitOpt& chosen, bool root_skipped = false) {
   CfrTree& T = cfr_lds(T_in);
   CfrState& S = cfr_lds(S_in);
   if (S.phase == CP_DONE) return 0;
   if (S.phase == CP_INIT) {
     S.orig = T.orig;
-    int root = cfr_node(T, *T.w0, -1, 0);
+    int root = cfr_node(T, *T.w0, -1, 0, root_skipped);
     S.root = root;
     S.it = 0;
     if (root < 0 || T.err || (T.nodes[root].flags & NF_TERMINAL)) {
@@ -799,14 +842,8 @@ CIT_HD int cfr_preorder_next(const CfrTree& T, int n, int top) {
 
 // The tree of lane l in a node pool (nodes | edges | rows per tree), read-only use.
 CIT_HD CfrTree cfr_tree_view(uint8_t* pool, long l, int node_cap, int edge_cap) {
-  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
-  uint8_t* base = pool + per * l;
   CfrTree T;
-  T.nodes = reinterpret_cast<CfrNode*>(base);
-  T.edges = reinterpret_cast<CfrEdge*>(base + (long)node_cap * sizeof(CfrNode));
-  T.rows = reinterpret_cast<uint32_t*>(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
-  T.node_cap = node_cap;
-  T.edge_cap = edge_cap;
+  cfr_tree_bind(T, pool, l, node_cap, edge_cap);
   return T;
 }
 
@@ -860,10 +897,11 @@ CIT_HD void cfr_emit_targets(const CfrTree& T, CitMT& py, int root, int mode, in
     m[4] = c;
     if (feat) cit_encode_game(g, feat + (long)t * CIT_FEAT, pid);
     for (int k = 0; k < 6; k++) value[(long)t * 6 + k] = N.nv[k];
+    const CfrWide* W = (N.flags & NF_ROLE_PICK) ? cfr_wide(T, N.first_edge) : nullptr;
     bool zero = true;
-    for (int j = 0; j < N.n_children; j++) zero = zero && E[j].R[row] == 0.0;
+    for (int j = 0; j < N.n_children; j++) zero = zero && (W ? W[j].R[row] : E[j].R) == 0.0;
     for (int j = 0; j < N.n_children; j++) {
-      dist[c + j] = zero ? 1.0 : E[j].R[row];
+      dist[c + j] = zero ? 1.0 : (W ? W[j].R[row] : E[j].R);
       cit_encode_option(E[j].opt, g, opt_feat + (long)(c + j) * CIT_OPT_FEAT);
     }
     c += N.n_children;

@@ -30,7 +30,8 @@ __device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, 
 // One MCCFR decision per workgroup: a 64-lane team runs the search on its
 // tree (node pool in HBM, working rows in LDS).
 __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
-                                                   uint32_t* npidx, uint64_t* seer, int B, int iters, uint8_t* pool,
+                                                   uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
+                                                   const int32_t* orig, uint8_t* pool,
                                                    int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen,
                                                    int32_t* stats) {
   __shared__ __attribute__((aligned(16))) uint32_t w0s[ROW_W];
@@ -39,14 +40,8 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   __shared__ __attribute__((aligned(16))) CitOpt lbufs[CFR_LBUF];
   long l = blockIdx.x;
   if (l >= B) return;
-  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
-  uint8_t* base = pool + per * l;
   __shared__ CfrTree T;     // shared: the wavefront's lanes update it in lockstep
-  T.nodes = reinterpret_cast<CfrNode*>(base);
-  T.edges = reinterpret_cast<CfrEdge*>(base + (long)node_cap * sizeof(CfrNode));
-  T.rows = reinterpret_cast<uint32_t*>(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
-  T.node_cap = node_cap;
-  T.edge_cap = edge_cap;
+  cfr_tree_bind(T, pool, l, node_cap, edge_cap);
   T.n_nodes = T.n_edges = 0;
   T.training = false;
   __shared__ uint32_t pys[CIT_MT_N], nps[CIT_MT_N];
@@ -61,8 +56,8 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   T.err = 0;
   T.carry_outs = 0;
   copy_row(T, w0s, games + l * ROW_W);
-  T.orig = T.w0->gs_pid;
-  int root = cfr_train(T, iters);
+  T.orig = orig ? orig[l] : T.w0->gs_pid;
+  int root = cfr_train(T, iters, (flags & CIT_CFR_ROOT_SKIPPED) != 0);
   CitOpt c = mk(O_NUM_NAMES, 0);
   if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
   if (root >= 0) copy_row(T, games + l * ROW_W, row_of(T, root));
@@ -83,8 +78,8 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
 // One resumption of cfr_pred (cit_cfr.h: cfr_pred_run) per tree; lane 0 adds
 // 1 to *waiting when the tree suspends for a leaf evaluation.
 __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
-                                                      uint32_t* npidx, uint64_t* seer, int B, int iters, int max_depth,
-                                                      uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
+                                                      uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
+                                                      const int32_t* orig, int max_depth, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
                                                       CfrState* state, const float* probs, float* feat,
                                                       CitOpt* chosen, int32_t* waiting) {
   __shared__ __attribute__((aligned(16))) uint32_t w0s[ROW_W];
@@ -96,14 +91,8 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   __shared__ CfrState S;
   S = state[l];             // every lane stores the same value
   if (S.phase == CP_DONE) return;
-  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
-  uint8_t* base = pool + per * l;
   __shared__ CfrTree T;     // shared: the wavefront's lanes update it in lockstep
-  T.nodes = reinterpret_cast<CfrNode*>(base);
-  T.edges = reinterpret_cast<CfrEdge*>(base + (long)node_cap * sizeof(CfrNode));
-  T.rows = reinterpret_cast<uint32_t*>(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
-  T.node_cap = node_cap;
-  T.edge_cap = edge_cap;
+  cfr_tree_bind(T, pool, l, node_cap, edge_cap);
   T.training = false;
   __shared__ uint32_t pys[CIT_MT_N], nps[CIT_MT_N];
   T.py = mt_stage_in(pys, mt, idx, B, l);
@@ -119,12 +108,13 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
     T.err = 0;
     T.carry_outs = 0;
     copy_row(T, w0s, games + l * ROW_W);
-    T.orig = T.w0->gs_pid;
+    T.orig = orig ? orig[l] : T.w0->gs_pid;
   } else {
     cfr_state_load(T, S);
   }
   CitOpt c;
-  int r = cfr_pred_run(T, S, iters, max_depth, probs + 6 * l, feat + (long)CIT_FEAT * l, c);
+  int r = cfr_pred_run(T, S, iters, max_depth, probs + 6 * l, feat + (long)CIT_FEAT * l, c,
+                       (flags & CIT_CFR_ROOT_SKIPPED) != 0);
   cfr_state_save(T, S);
   if (!r && S.root >= 0) copy_row(T, games + l * ROW_W, row_of(T, S.root));
   mt_stage_out(pys, mt, B, l);
@@ -148,34 +138,34 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
 
 extern "C" {
 
-int cit_cfr_pool_bytes(int node_cap, int edge_cap) {
-  long b = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
-  return b > 0x7fffffff ? -1 : (int)b;
+int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap) {
+  if (node_cap <= 0 || edge_cap <= 0) return -1;
+  return cfr_pool_bytes(node_cap, edge_cap);
 }
 int cit_cfr_opt_cap(void) { return CFR_OPT_CAP; }
 
 int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
-                   int B, int iters, void* pool, int node_cap, int edge_cap, CitOption* optbuf, CitOption* chosen,
-                   int32_t* stats, hipStream_t stream) {
+                   int B, int iters, int flags, const int32_t* orig_player, void* pool, int node_cap, int edge_cap,
+                   CitOption* optbuf, CitOption* chosen, int32_t* stats, hipStream_t stream) {
   if (B <= 0 || iters < 0 || node_cap <= 0 || edge_cap <= 0 || !games || !mt || !mt_idx || !np_mt || !np_idx ||
       !seer || !pool || !optbuf || !chosen || !stats)
     return -1;
   hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
-                     B, iters, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats);
+                     B, iters, flags, orig_player, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats);
   CHECK_LAUNCH();
 }
 
 int cit_cfr_state_bytes(void) { return (int)sizeof(CfrState); }
 
 int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
-                      int B, int iters, int max_depth, void* pool, int node_cap, int edge_cap, CitOption* optbuf,
-                      void* state, const float* probs, float* feat, CitOption* chosen, int32_t* waiting,
-                      hipStream_t stream) {
+                      int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,
+                      int node_cap, int edge_cap, CitOption* optbuf, void* state, const float* probs, float* feat,
+                      CitOption* chosen, int32_t* waiting, hipStream_t stream) {
   if (B <= 0 || iters < 0 || node_cap <= 0 || edge_cap <= 0 || !games || !mt || !mt_idx || !np_mt || !np_idx ||
       !seer || !pool || !optbuf || !state || !probs || !feat || !chosen || !waiting)
     return -1;
   hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
-                     seer, B, iters, max_depth, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
+                     seer, B, iters, flags, orig_player, max_depth, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
                      (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting);
   CHECK_LAUNCH();
 }

@@ -2127,6 +2127,27 @@ CIT_HD int cit_random_step(CitGame& g, CitMT& rng, uint64_t* seer) {
   return (w >= 0 || g.err || g.terminal) ? 1 : 0;
 }
 
+// skip_false_choice (deep_mccfr.py:37-49) on its own, for CFRNode(game)
+// constructed by the facade: auto-plays single-option steps (at most 101) and
+// stops at a winner.  Returns the number of carry_outs.
+CIT_HD int cit_skip_false_choice(CitGame& g, CitMT& py, uint64_t* seer) {
+  uint32_t e = 0;
+  cit_prepare_options(g, py, seer);
+  int n = cit_count_options(g, e, seer);
+  int i = 0;
+  bool done = false;
+  while (n == 1 && !done && !e && !g.err) {
+    i++;
+    CitOpt o = cit_pick_option(g, 0, seer);
+    done = cit_carry_out(g, o, py) >= 0;
+    cit_prepare_options(g, py, seer);
+    n = cit_count_options(g, e, seer);
+    if (i > 100) done = true;
+  }
+  g.err |= e;
+  return i;
+}
+
 // compare_to_random.play_games' step loop (compare_to_random.py:16-35) up to
 // the next searched decision.  Seats in `search_mask` decide by search when
 // they have more than one option; that test is one get_options call, and a

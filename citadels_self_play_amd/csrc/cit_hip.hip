@@ -123,6 +123,42 @@ __global__ __launch_bounds__(64) void k_get_options(uint32_t* games, uint32_t* m
   });
 }
 
+// Agent.get_options' count only (get_options may mutate the game: state 9
+// scholar picks, state 8 seer draws), nothing materialised.
+__global__ __launch_bounds__(64) void k_count_options(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer,
+                                                     int B, int32_t* n_opts) {
+  uniform_game<false, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
+    uint64_t* sc = seer + l * CIT_SEER_MAX;
+    cit_prepare_options(g, r, sc);
+    uint32_t e = 0;
+    n_opts[l] = cit_count_options(g, e, sc);
+    g.err |= e;
+  });
+}
+
+// Game.sample_private_information(players[orig[l]], role_sample) per lane.
+__global__ __launch_bounds__(64) void k_determinize(uint32_t* games, uint32_t* mt, uint32_t* idx, int B,
+                                                   const int32_t* orig, int role_sample) {
+  __shared__ __attribute__((aligned(16))) uint8_t unk[CIT_USED_CAP + 48];
+  uniform_game<false, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
+    int o = orig[l];
+    if (o < 0 || o >= CIT_NP) {
+      g.err |= CIT_ERR_INDEX;
+      return;
+    }
+    cit_sample_private(g, o, role_sample != 0, r, unk);
+  });
+}
+
+// CFRNode.skip_false_choice (deep_mccfr.py:37-49) per lane; carried[l] = steps played.
+__global__ __launch_bounds__(64) void k_skip_false_choice(uint32_t* games, uint32_t* mt, uint32_t* idx,
+                                                         uint64_t* seer, int B, int32_t* carried) {
+  uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
+    int n = cit_skip_false_choice(g, r, seer + l * CIT_SEER_MAX);
+    if (carried) carried[l] = n;
+  });
+}
+
 __global__ __launch_bounds__(64) void k_carry_out(uint32_t* games, uint32_t* mt, uint32_t* idx, int B,
                                                  const CitOpt* chosen, int32_t* winner) {
   uniform_game<false, true>(games, mt, idx, B,
@@ -272,7 +308,7 @@ int cit_roll_prof_read(unsigned long long* out) {
 }
 #endif
 
-int cit_abi_version(void) { return 1; }
+int cit_abi_version(void) { return 2; }
 int cit_game_bytes(void) { return CIT_GAME_BYTES; }
 int cit_seer_scratch_words(void) { return CIT_SEER_MAX; }
 
@@ -316,6 +352,29 @@ int cit_get_options(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer,
   if (B <= 0 || max_opts < 0 || !games || !mt || !mt_idx || !seer || !n_opts || (max_opts && !opts)) return -1;
   hipLaunchKernelGGL(k_get_options, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt,
                      mt_idx, seer, B, (CitOpt*)opts, max_opts, n_opts);
+  CHECK_LAUNCH();
+}
+
+int cit_count_options(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int32_t* n_opts,
+                      hipStream_t stream) {
+  if (B <= 0 || !games || !mt || !mt_idx || !seer || !n_opts) return -1;
+  hipLaunchKernelGGL(k_count_options, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, seer, B, n_opts);
+  CHECK_LAUNCH();
+}
+
+int cit_determinize(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const int32_t* orig_player, int role_sample,
+                    hipStream_t stream) {
+  if (B <= 0 || !games || !mt || !mt_idx || !orig_player) return -1;
+  hipLaunchKernelGGL(k_determinize, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, B, orig_player,
+                     role_sample);
+  CHECK_LAUNCH();
+}
+
+int cit_skip_false_choice(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int32_t* carried,
+                          hipStream_t stream) {
+  if (B <= 0 || !games || !mt || !mt_idx || !seer) return -1;
+  hipLaunchKernelGGL(k_skip_false_choice, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, seer, B,
+                     carried);
   CHECK_LAUNCH();
 }
 

@@ -145,6 +145,37 @@ void cith_advance_random(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer
   }
 }
 
+int64_t cith_cfr_pool_bytes(int node_cap, int edge_cap) { return cfr_pool_bytes(node_cap, edge_cap); }
+
+void cith_count_options(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int* n_opts) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    uint64_t* sc = seer + (long)l * CIT_SEER_MAX;
+    cit_prepare_options(g[l], r, sc);
+    uint32_t e = 0;
+    n_opts[l] = cit_count_options(g[l], e, sc);
+    g[l].err |= e;
+    SAVE(r);
+  }
+}
+
+void cith_determinize(CitGame* g, uint32_t* mt, uint32_t* idx, int B, const int* orig, int role_sample) {
+  uint8_t unk[CIT_USED_CAP + 48];
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    cit_sample_private(g[l], orig[l], role_sample != 0, r, unk);
+    SAVE(r);
+  }
+}
+
+void cith_skip_false_choice(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int* carried) {
+  for (int l = 0; l < B; l++) {
+    CitMT r = lane_rng(mt, idx, B, l);
+    carried[l] = cit_skip_false_choice(g[l], r, seer + (long)l * CIT_SEER_MAX);
+    SAVE(r);
+  }
+}
+
 int cith_cfr_sizes(int* out) {
   out[0] = (int)sizeof(CfrNode);
   out[1] = (int)sizeof(CfrEdge);
@@ -156,20 +187,14 @@ int cith_cfr_sizes(int* out) {
 // pool = per lane [node_cap CfrNode][edge_cap CfrEdge][node_cap rows].
 // stats[l] = {root, n_nodes, n_edges, carry_outs, err}
 void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx, uint64_t* seer, int B,
-                     int iters, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen, int* stats) {
-  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
+                     int iters, int flags, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen, int* stats) {
   CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   uint8_t tmp[128];
   CitOpt lbuf[CFR_LBUF];
   for (int l = 0; l < B; l++) {
-    uint8_t* base = pool + per * l;
     CfrTree T;
-    T.nodes = (CfrNode*)base;
-    T.edges = (CfrEdge*)(base + (long)node_cap * sizeof(CfrNode));
-    T.rows = (uint32_t*)(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
-    T.node_cap = node_cap;
-    T.edge_cap = edge_cap;
+    cfr_tree_bind(T, pool, l, node_cap, edge_cap);
     T.n_nodes = T.n_edges = 0;
     T.orig = g[l].gs_pid;
     T.training = false;
@@ -184,7 +209,7 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
     T.err = 0;
     T.carry_outs = 0;
     memcpy(w0, &g[l], CIT_GAME_BYTES);
-    int root = cfr_train(T, iters);
+    int root = cfr_train(T, iters, (flags & 1) != 0);
     CitOpt c = mk(O_NUM_NAMES, 0);
     if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
     chosen[l] = c;
@@ -213,7 +238,6 @@ void cith_encode_options(const CitGame* g, const CitOpt* opts, int n, float* out
 int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx, uint64_t* seer,
                        int B, int iters, int max_depth, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
                        CfrState* st, const float* probs, float* feat, CitOpt* chosen) {
-  long per = (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge) + (long)node_cap * CIT_GAME_BYTES;
   CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   uint8_t tmp[128];
@@ -222,13 +246,8 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
   for (int l = 0; l < B; l++) {
     CfrState& S = st[l];
     if (S.phase == CP_DONE) continue;
-    uint8_t* base = pool + per * l;
     CfrTree T;
-    T.nodes = (CfrNode*)base;
-    T.edges = (CfrEdge*)(base + (long)node_cap * sizeof(CfrNode));
-    T.rows = (uint32_t*)(base + (long)node_cap * sizeof(CfrNode) + (long)edge_cap * sizeof(CfrEdge));
-    T.node_cap = node_cap;
-    T.edge_cap = edge_cap;
+    cfr_tree_bind(T, pool, l, node_cap, edge_cap);
     T.training = false;
     T.py = lane_rng(mt, idx, B, l);
     T.np = lane_rng(npmt, npidx, B, l);

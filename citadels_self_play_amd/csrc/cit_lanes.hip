@@ -88,6 +88,25 @@ __global__ void k_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, 
   idx[l] = r.pos;
 }
 
+// CFRNode.action_choice(live=False) (deep_mccfr.py:67-91) at node[l] of tree
+// l: the child's edge index (np.random.choice from the tree's numpy stream),
+// -1 with err[l] set when numpy would raise.
+__global__ void k_cfr_choose(uint8_t* pool, int B, int node_cap, int edge_cap, const int32_t* node, uint32_t* npmt,
+                             uint32_t* npidx, int32_t* edge_out, int32_t* err_out) {
+  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= B) return;
+  CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+  T.np = lane_mt(npmt, npidx, B, l);
+  T.err = 0;
+  int n = node[l];
+  int a = -1;
+  if (n < 0 || n >= node_cap || T.nodes[n].n_children <= 0) T.err |= CIT_ERR_VALUE;   // choice over []
+  else a = cfr_choose(T, n);
+  edge_out[l] = T.err ? -1 : a;
+  err_out[l] = (int32_t)T.err;
+  npidx[l] = T.np.pos;
+}
+
 size_t lds_bytes(int G) { return (size_t)G * LDS_W * 4; }
 
 bool g_attrs_done = false;
@@ -134,6 +153,14 @@ int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t
     return -1;
   hipLaunchKernelGGL(k_cfr_targets, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap, edge_cap,
                      roots, mode, mt, mt_idx, offsets, meta, feat, value, dist, opt_feat);
+  CHECK_LAUNCH();
+}
+
+int cit_cfr_action_choice(void* pool, int B, int node_cap, int edge_cap, const int32_t* node, uint32_t* np_mt,
+                          uint32_t* np_idx, int32_t* edge, int32_t* err, hipStream_t stream) {
+  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !node || !np_mt || !np_idx || !edge || !err) return -1;
+  hipLaunchKernelGGL(k_cfr_choose, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap, edge_cap,
+                     node, np_mt, np_idx, edge, err);
   CHECK_LAUNCH();
 }
 

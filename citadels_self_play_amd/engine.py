@@ -22,8 +22,33 @@ NODE_DT = np.dtype([("parent", "<i4"), ("first_edge", "<i4"), ("n_children", "<i
                     ("depth", "<i2"), ("player", "i1"), ("gs_state", "i1"), ("flags", "u1"), ("winner", "i1"),
                     ("pad", "u1", 6), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
 ERR_OVERFLOW = 0x1         # CIT_ERR_OVERFLOW (csrc/cit_core.h)
-EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8", 6), ("S", "<f8", 6),
-                    ("CS", "<f8", 6)])
+EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8"), ("S", "<f8"), ("CS", "<f8")])
+WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])   # role-pick columns (csrc/cit_cfr.h)
+CFR_ROOT_SKIPPED = 1       # CIT_CFR_ROOT_SKIPPED (include/citadels.h)
+
+
+def node_arrays(nodes, edges, n):
+    """(cumulative_regrets, strategy, cumulative_strategy) of node n in the
+    reference's shapes: [nch] for a normal node, [6, 10] for a role-pick node
+    (whose [6]-wide columns follow its 10 edges in the pool)."""
+    N = nodes[n]
+    nch, f = int(N["n_children"]), int(N["first_edge"])
+    if nch == 0:
+        return np.zeros(0), np.zeros(0), np.zeros(0)
+    if N["flags"] & 1:
+        W = edges[f + 10:f + 40].view(WIDE_DT)[:nch]
+        return W["R"].T.copy(), W["S"].T.copy(), W["CS"].T.copy()
+    E = edges[f:f + nch]
+    return E["R"].copy(), E["S"].copy(), E["CS"].copy()
+
+
+def pool_caps(iters):
+    """Node / edge capacity for a cfr_train(iters) tree: measured 1.8-2.3
+    nodes and 3.5-4.4 reserved edge slots per node at 2k-200k iterations
+    (tools/cfr_tree_sizes.py); a tree that still outgrows its pool is searched
+    again with a 4x pool (GameBatch._retry_overflow)."""
+    node_cap = max(1024, int(2.5 * iters) + 256)
+    return node_cap, 5 * node_cap
 
 
 def _ptr(t):
@@ -137,7 +162,7 @@ class GameBatch:
         return tuple(t.clone() for t in (self.games, self.mt, self.mt_idx, self.seer, self.np_mt, self.np_idx,
                                          self.steps))
 
-    def _retry_overflow(self, snap, stats, chosen, run, max_retries):
+    def _retry_overflow(self, snap, stats, chosen, run, max_retries, orig=None):
         """Lanes whose search overflowed its node / edge pool (stats err bit
         CIT_ERR_OVERFLOW) are searched again from their pre-search state with a
         4x larger pool; results and streams are scattered back, and the
@@ -150,7 +175,9 @@ class GameBatch:
         sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),
                                      seer[over].contiguous(), npm[:, over].contiguous(), npi[over].contiguous())
         sub.steps = steps[over].contiguous()
-        c2, s2 = run(sub, 4 * self.node_cap, 4 * self.edge_cap, max_retries - 1)
+        sub_orig = None if orig is None else \
+            np.broadcast_to(np.asarray(orig, np.int32), (self.B,))[over.cpu().numpy()].copy()
+        c2, s2 = run(sub, 4 * self.node_cap, 4 * self.edge_cap, max_retries - 1, sub_orig)
         self.scatter(sub, over)
         chosen = chosen.clone()
         stats = stats.clone()
@@ -159,7 +186,7 @@ class GameBatch:
         self._retry = (over, sub)
         return chosen, stats
 
-    def cfr_decide(self, iters, node_cap=1024, edge_cap=None, max_retries=3):
+    def cfr_decide(self, iters, node_cap=1024, edge_cap=None, max_retries=3, flags=0, orig=None):
         """run_mccfr(game, max_iterations=iters) (no model) on every lane; returns
         (chosen [B,16] uint8 descriptors, stats [B,5] = root, nodes, edges, carry_outs, err).
         A tree that outgrows its pool is searched again with a 4x pool (up to
@@ -167,17 +194,26 @@ class GameBatch:
         if not hasattr(self, "np_mt"):
             self.seed_numpy()
         snap = self._snapshot() if max_retries > 0 else None
-        chosen, stats = self._cfr_decide(iters, node_cap, edge_cap)
+        chosen, stats = self._cfr_decide(iters, node_cap, edge_cap, flags, orig)
         return self._retry_overflow(snap, stats, chosen,
-                                    lambda sub, nc, ec, mr: sub.cfr_decide(iters, nc, ec, mr), max_retries)
+                                    lambda sub, nc, ec, mr, o: sub.cfr_decide(iters, nc, ec, mr, flags, o),
+                                    max_retries, orig)
 
-    def _cfr_decide(self, iters, node_cap, edge_cap):
+    def _orig(self, orig):
+        """CFRNode's original_player_id per lane as a device int32 tensor (None: the game's own)."""
+        if orig is None:
+            return None
+        return torch.as_tensor(np.broadcast_to(np.asarray(orig, np.int32), (self.B,)).copy()).to(self.device)
+
+    def _cfr_decide(self, iters, node_cap, edge_cap, flags=0, orig=None):
         self._pool(node_cap, edge_cap)
         node_cap, edge_cap = self.node_cap, self.edge_cap
+        o = self._orig(orig)
         chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
         stats = torch.zeros((self.B, 5), dtype=torch.int32, device=self.device)
         _lib.check(self.lib.cit_cfr_decide(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt),
-                                           _ptr(self.np_idx), _ptr(self.seer), self.B, int(iters), _ptr(self.pool),
+                                           _ptr(self.np_idx), _ptr(self.seer), self.B, int(iters), int(flags),
+                                           None if o is None else _ptr(o), _ptr(self.pool),
                                            node_cap, edge_cap, _ptr(self.optbuf), _ptr(chosen), _ptr(stats),
                                            _stream()), "cit_cfr_decide")
         return chosen, stats
@@ -280,17 +316,21 @@ class GameBatch:
         return out
 
     def _pool(self, node_cap, edge_cap):
-        edge_cap = edge_cap or 8 * node_cap
+        edge_cap = edge_cap or 5 * node_cap
         per = self.lib.cit_cfr_pool_bytes(node_cap, edge_cap)
-        if per <= 0:
-            raise ValueError("node pool too large per tree")
+        if per <= 0 or node_cap >= 2 ** 31 or edge_cap >= 2 ** 31:
+            raise ValueError("bad node pool capacity (%d nodes, %d edges)" % (node_cap, edge_cap))
         need = per * self.B
+        if getattr(self, "pool", None) is not None and self.pool.numel() < need:
+            self.pool = None                        # free the old pool before allocating the new one
+            torch.cuda.empty_cache()
         if getattr(self, "pool", None) is None or self.pool.numel() < need:
             self.pool = torch.empty(need, dtype=torch.uint8, device=self.device)
             self.optbuf = torch.empty((self.B, self.lib.cit_cfr_opt_cap(), 16), dtype=torch.uint8, device=self.device)
         self.node_cap, self.edge_cap = node_cap, edge_cap
 
-    def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000, max_retries=3):
+    def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000, max_retries=3,
+                 flags=0, orig=None):
         """run_mccfr(game, model, max_iterations=iters) with a model and training=False
         (cfr_pred(iters, max_depth) + live action choice) on every lane.  `net` is a
         models.ValueNet; leaf rows of all suspended trees are evaluated in one MFMA
@@ -299,19 +339,20 @@ class GameBatch:
         if not hasattr(self, "np_mt"):
             self.seed_numpy()
         snap = self._snapshot() if max_retries > 0 else None
-        chosen, stats, rounds = self._cfr_pred(iters, net, max_depth, node_cap, edge_cap, max_rounds)
+        chosen, stats, rounds = self._cfr_pred(iters, net, max_depth, node_cap, edge_cap, max_rounds, flags, orig)
         box = [rounds]
 
-        def run(sub, nc, ec, mr):
-            c, st, r = sub.cfr_pred(iters, net, max_depth, nc, ec, max_rounds, mr)
+        def run(sub, nc, ec, mr, o):
+            c, st, r = sub.cfr_pred(iters, net, max_depth, nc, ec, max_rounds, mr, flags, o)
             box[0] += r
             return c, st
-        chosen, stats = self._retry_overflow(snap, stats, chosen, run, max_retries)
+        chosen, stats = self._retry_overflow(snap, stats, chosen, run, max_retries, orig)
         return chosen, stats, box[0]
 
-    def _cfr_pred(self, iters, net, max_depth, node_cap, edge_cap, max_rounds):
+    def _cfr_pred(self, iters, net, max_depth, node_cap, edge_cap, max_rounds, flags=0, orig=None):
         self._pool(node_cap, edge_cap)
         d = self.device
+        o = self._orig(orig)
         state = torch.zeros((self.B, self.lib.cit_cfr_state_bytes() // 4), dtype=torch.int32, device=d)
         feat = torch.zeros((self.B, 418), dtype=torch.float32, device=d)
         probs = torch.zeros((self.B, 6), dtype=torch.float32, device=d)
@@ -323,7 +364,9 @@ class GameBatch:
             waiting.zero_()
             _lib.check(self.lib.cit_cfr_pred_step(
                 _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
-                _ptr(self.seer), self.B, int(iters), int(max_depth), _ptr(self.pool), self.node_cap, self.edge_cap,
+                _ptr(self.seer), self.B, int(iters), int(flags), None if o is None else _ptr(o), int(max_depth),
+                _ptr(self.pool), self.node_cap,
+                self.edge_cap,
                 _ptr(self.optbuf), _ptr(state), _ptr(probs), _ptr(feat), _ptr(chosen), _ptr(waiting), _stream()),
                 "cit_cfr_pred_step")
             if int(waiting.item()) == 0:
@@ -339,11 +382,33 @@ class GameBatch:
         """(nodes, edges, rows) numpy views of one lane's search tree (host copy)."""
         per = self.lib.cit_cfr_pool_bytes(self.node_cap, self.edge_cap)
         base = self.pool[lane * per:(lane + 1) * per].cpu().numpy()
-        nc, ec = self.node_cap, self.edge_cap
-        nodes = base[:nc * 168].view(NODE_DT)
-        edges = base[nc * 168:nc * 168 + ec * 168].view(EDGE_DT)
-        rows = base[nc * 168 + ec * 168:].reshape(nc, L.GAME_BYTES)
+        nb, eb = self.node_cap * NODE_DT.itemsize, self.edge_cap * EDGE_DT.itemsize
+        nodes = base[:nb].view(NODE_DT)
+        edges = base[nb:nb + eb].view(EDGE_DT)
+        rows = base[nb + eb:].reshape(self.node_cap, L.GAME_BYTES)
         return nodes, edges, rows
+
+    # --- single-game pieces of the search, exposed for the object API -------------
+    def count_options(self):
+        """len(get_options_from_state()) per lane (cit_count_options; may mutate like get_options)."""
+        n = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_count_options(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.seer),
+                                              self.B, _ptr(n), _stream()), "cit_count_options")
+        return n
+
+    def determinize(self, orig_player, role_sample=True):
+        """Game.sample_private_information(players[orig], role_sample) per lane."""
+        o = torch.as_tensor(np.broadcast_to(np.asarray(orig_player, np.int32), (self.B,)).copy()).to(self.device)
+        _lib.check(self.lib.cit_determinize(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), self.B, _ptr(o),
+                                            int(bool(role_sample)), _stream()), "cit_determinize")
+
+    def skip_false_choice(self):
+        """CFRNode.skip_false_choice on every lane's game; returns carry_outs played."""
+        c = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_skip_false_choice(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx),
+                                                  _ptr(self.seer), self.B, _ptr(c), _stream()),
+                   "cit_skip_false_choice")
+        return c
 
     # --- inspection --------------------------------------------------------------
     def rows(self):

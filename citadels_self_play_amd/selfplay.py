@@ -27,7 +27,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .engine import GameBatch
+from .engine import GameBatch, pool_caps
 
 TARGET_ROW_BYTES = 418 * 4 + 6 * 8      # encode_game f32[418] | node_value f64[6]
 
@@ -39,10 +39,14 @@ def init_distributed():
     to rehearse N ranks on a one-GPU box; the product path is RCCL."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    n_dev = torch.cuda.device_count()
+    backend = os.environ.get("CIT_DIST_BACKEND", "nccl")
+    if ws > 1 and backend == "nccl" and ws > n_dev:
+        raise RuntimeError("WORLD_SIZE=%d ranks but %d visible GPUs: RCCL runs one rank per GPU "
+                           "(CIT_DIST_BACKEND=gloo only rehearses folded ranks)" % (ws, n_dev))
+    dev = torch.device("cuda", local % max(1, n_dev))
     torch.cuda.set_device(dev)
     if ws > 1 and not dist.is_initialized():
-        backend = os.environ.get("CIT_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -90,18 +94,62 @@ def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None):
     return b, chosen, stats, rounds
 
 
-def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_cap=None):
+def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_cap=None, max_pool_bytes=None,
+                   log=None):
     """simulate_game (train_from_scratch.py:23-36, pretrain / training=True: the
     search ignores the model) for every seed: random.seed(s), np.random.seed(s),
     create_a_random_game(max_move), run_mccfr(iters, training=True),
-    get_all_targets.  Returns (batch, stats, targets dict of device tensors)."""
-    b = GameBatch(seeds, preset=True, device=device)
-    b.random_position(max_move)
-    b.seed_numpy()
-    cap = node_cap or max(1024, 4 * iters)
-    chosen, stats = b.cfr_decide(iters, node_cap=cap, edge_cap=edge_cap)
-    targets = b.cfr_targets(stats[:, 0], mode=0)
-    return b, stats, targets
+    get_all_targets.  Returns (batch, stats, targets dict of device tensors).
+
+    Node pools are sized from `iters` (engine.pool_caps: a cfr_train(200000)
+    tree takes ~0.5-1 GB); when the seeds' pools do not fit in
+    `max_pool_bytes` (default: 60 % of the free device memory) the seeds run in
+    consecutive chunks and the results are concatenated in seed order (the
+    returned batch is then the last chunk's)."""
+    from . import _lib
+    if node_cap is None:
+        node_cap, ec = pool_caps(iters)
+        edge_cap = edge_cap or ec
+    edge_cap = edge_cap or 5 * node_cap
+    dev = torch.device(device or "cuda")
+    per = _lib.load().cit_cfr_pool_bytes(node_cap, edge_cap)
+    if max_pool_bytes is None:
+        max_pool_bytes = int(0.6 * torch.cuda.mem_get_info(dev)[0])
+    seeds = np.asarray(seeds, np.int64)
+    chunk = int(max(1, min(len(seeds), max_pool_bytes // max(per, 1))))
+    parts = []
+    b = None
+    for i in range(0, len(seeds), chunk):
+        if b is not None:
+            b.pool = None                      # free the previous chunk's trees
+        b = GameBatch(seeds[i:i + chunk], preset=True, device=dev)
+        b.random_position(max_move)
+        b.seed_numpy()
+        chosen, stats = b.cfr_decide(iters, node_cap=node_cap, edge_cap=edge_cap)
+        parts.append((stats, b.cfr_targets(stats[:, 0], mode=0)))
+        if log is not None and len(seeds) > chunk:
+            log("simulate_games: trees %d-%d of %d done" % (i, i + b.B - 1, len(seeds)))
+    if len(parts) == 1:
+        return b, parts[0][0], parts[0][1]
+    return b, torch.cat([p[0] for p in parts]), concat_targets([p[1] for p in parts], [p[0].shape[0] for p in parts])
+
+
+def concat_targets(ts, sizes):
+    """cfr_targets dicts of consecutive lane chunks -> one dict (lane and option
+    row indices shifted)."""
+    lane0, row0 = 0, 0
+    metas = []
+    for t, n in zip(ts, sizes):
+        m = t["meta"].clone()
+        m[:, 0] += lane0
+        m[:, 4] += row0
+        metas.append(m)
+        lane0 += n
+        row0 += t["dist"].shape[0]
+    out = {"meta": torch.cat(metas)}
+    for k in ("feat", "value", "dist", "opt_feat", "counts"):
+        out[k] = torch.cat([t[k] for t in ts])
+    return out
 
 
 def setup_games(seeds, iters, node_cap=None, device=None):
@@ -117,7 +165,8 @@ def setup_games(seeds, iters, node_cap=None, device=None):
     _lib.check(b.lib.cit_encode_games(b.games.data_ptr(), b.B, -1, feat.data_ptr(),
                                       torch.cuda.current_stream(b.device).cuda_stream), "cit_encode_games")
     b.seed_numpy()
-    chosen, stats = b.cfr_decide(iters, node_cap=node_cap or max(1024, 4 * iters))
+    nc, ec = pool_caps(iters)
+    chosen, stats = b.cfr_decide(iters, node_cap=node_cap or nc, edge_cap=None if node_cap else ec)
     targets = b.cfr_targets(stats[:, 0], mode=1)
     return b, feat, stats, targets
 

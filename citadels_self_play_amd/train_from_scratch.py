@@ -34,7 +34,7 @@ def collect(rank, world, args, phase, min_targets, log):
         base = args.seed + (phase * 1000 + rnd) * args.games_per_gpu * world
         seeds = selfplay.shard(args.games_per_gpu * world, base_seed=base)
         t0 = time.time()
-        b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap)
+        b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap, log=log)
         f, v = selfplay.all_gather_targets(t["feat"], t["value"])
         feats.append(f.cpu())
         values.append(v.cpu())

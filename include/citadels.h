@@ -48,7 +48,7 @@ typedef struct CitOption {
   uint64_t x;
 } CitOption;
 
-int cit_abi_version(void);
+int cit_abi_version(void);              /* 2: 48-B CfrEdge, 64-bit pool bytes, search flags */
 int cit_game_bytes(void);              /* row width of `games` */
 int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
 int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
@@ -78,6 +78,21 @@ int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t*
  * (scholar state 9, seer state 8). */
 int cit_get_options(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, CitOption* opts,
                     int max_opts, int32_t* n_opts, hipStream_t stream);
+
+/* len(Game.get_options_from_state()) for every lane, counted without
+ * materialising the list (the random-role cardinal / magician lists run into
+ * thousands; closed-form counts).  Same mutations and stream use as
+ * cit_get_options. */
+int cit_count_options(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int32_t* n_opts,
+                      hipStream_t stream);
+
+/* Game.sample_private_information(players[orig_player[l]], role_sample)
+ * (game/game.py:215-339; called by deep_mccfr.py:140,158): MCCFR
+ * determinization of every lane's game from that player's point of view,
+ * drawing from the lane's CPython stream.  An orig_player outside 0..5 sets
+ * the lane's IndexError bit. */
+int cit_determinize(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const int32_t* orig_player, int role_sample,
+                    hipStream_t stream);
 
 /* random.choice(options) for every lane (compare_to_random.py:38,
  * run_utils.py:39; Lib/random.py:371-373): k = _randbelow(n_opts[l]) drawn
@@ -123,15 +138,31 @@ int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1,
 
 /* --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------ */
 
-/* Bytes of node pool per tree: node_cap CfrNode (168 B) + edge_cap CfrEdge
- * (168 B) + node_cap packed game rows.  Opponent nodes reserve 10 edges. */
-int cit_cfr_pool_bytes(int node_cap, int edge_cap);
+/* Bytes of node pool per tree (64-bit: a cfr_train(200000) tree needs ~1 GB):
+ * node_cap CfrNode (168 B) + edge_cap CfrEdge (48 B) + node_cap packed game
+ * rows.  Opponent nodes reserve 10 edges, role-pick nodes 40 slots (10 edges +
+ * their [6]-wide regret / strategy columns).  -1 on a bad capacity. */
+int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap);
 int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */
 
 /* The config-3 position harness: k = random.randint(lo, hi) drawn from the
  * lane's stream, then k random-policy steps (stops at a winner). */
 int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int lo, int hi,
                        int32_t* steps, hipStream_t stream);
+
+/* `flags` of the search entry points: CIT_CFR_ROOT_SKIPPED = the lane's game
+ * already went through CFRNode.__init__'s skip_false_choice
+ * (cit_skip_false_choice), so the root node is built from it as is.
+ * `orig_player` [B] = CFRNode's original_player_id per lane, or NULL for the
+ * game's current player before the root's skip_false_choice (run_mccfr). */
+#define CIT_CFR_ROOT_SKIPPED 1
+
+/* CFRNode.skip_false_choice() (algorithms/deep_mccfr.py:37-49) on every lane,
+ * as the CFRNode constructor runs it on the game it is given (:19-20):
+ * single-option steps are played (at most 101) until a choice or a winner.
+ * carried[l] (may be NULL) = carry_outs played. */
+int cit_skip_false_choice(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int32_t* carried,
+                          hipStream_t stream);
 
 /* run_mccfr(game, max_iterations=iters) without a model (run_utils.py:74-87):
  * CFRNode(game) (deep_mccfr.py:8-49) + cfr_train(iters) (:187-205) +
@@ -143,8 +174,8 @@ int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
  * {root node, nodes, edges, carry_out calls, error bits}.  The tree stays in
  * pool (B x cit_cfr_pool_bytes) for inspection / target extraction. */
 int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
-                   int B, int iters, void* pool, int node_cap, int edge_cap, CitOption* optbuf, CitOption* chosen,
-                   int32_t* stats, hipStream_t stream);
+                   int B, int iters, int flags, const int32_t* orig_player, void* pool, int node_cap, int edge_cap,
+                   CitOption* optbuf, CitOption* chosen, int32_t* stats, hipStream_t stream);
 
 /* Deep MCCFR with value-net leaves: cfr_pred(iters, max_depth)
  * (deep_mccfr.py:207-229) as run_mccfr runs it with a model and training=False
@@ -157,9 +188,9 @@ int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt,
  * once per node (the reference recomputes the same value). */
 int cit_cfr_state_bytes(void);
 int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
-                      int B, int iters, int max_depth, void* pool, int node_cap, int edge_cap, CitOption* optbuf,
-                      void* state, const float* probs, float* feat, CitOption* chosen, int32_t* waiting,
-                      hipStream_t stream);
+                      int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,
+                      int node_cap, int edge_cap, CitOption* optbuf, void* state, const float* probs, float* feat,
+                      CitOption* chosen, int32_t* waiting, hipStream_t stream);
 
 /* compare_to_random.play_games' step loop (compare_to_random.py:16-35) on
  * every lane up to its next searched decision: seats in search_mask (bit p =
@@ -194,6 +225,15 @@ int cit_random_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* s
 int cit_close_rows(void);
 int cit_close_position(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, uint32_t* store,
                        int32_t* index, hipStream_t stream);
+
+/* CFRNode.action_choice(live=False) (algorithms/deep_mccfr.py:67-91) at node
+ * node[l] of the finished tree of lane l (the in-search sampler: a normal node
+ * draws from cumulative_strategy / sum, a role-pick node from the pick-order
+ * weighted average, with np.random.choice on the lane's numpy stream).
+ * edge[l] = the chosen child's index within the node, or -1 with err[l] set
+ * (ValueError: no children / invalid probabilities). */
+int cit_cfr_action_choice(void* pool, int B, int node_cap, int edge_cap, const int32_t* node, uint32_t* np_mt,
+                          uint32_t* np_idx, int32_t* edge, int32_t* err, hipStream_t stream);
 
 /* get_all_targets (deep_mccfr.py:258-274) / build_train_targets (:321-345)
  * over the finished trees of cit_cfr_decide (same pool, roots = stats[:,0];

@@ -83,13 +83,27 @@ class HostBatch:
 NODE_DT = np.dtype([("parent", "<i4"), ("first_edge", "<i4"), ("n_children", "<i2"), ("edge_cap", "<i2"),
                     ("depth", "<i2"), ("player", "i1"), ("gs_state", "i1"), ("flags", "u1"), ("winner", "i1"),
                     ("pad", "u1", 6), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
-EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8", 6), ("S", "<f8", 6),
-                    ("CS", "<f8", 6)])
-assert NODE_DT.itemsize == 168 and EDGE_DT.itemsize == 168
+EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8"), ("S", "<f8"), ("CS", "<f8")])
+WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])
+assert NODE_DT.itemsize == 168 and EDGE_DT.itemsize == 48 and WIDE_DT.itemsize == 3 * 48
 
 
 def cfr_pool_bytes(node_cap, edge_cap):
-    return node_cap * 168 + edge_cap * 168 + node_cap * L.GAME_BYTES
+    return node_cap * 168 + edge_cap * 48 + node_cap * L.GAME_BYTES
+
+
+def node_arrays(nodes, edges, n):
+    """(R, S, CS) of node n as the reference holds them: [nch] for a normal
+    node, [6, 10] for a role-pick node (its wide records follow its 10 edges)."""
+    N = nodes[n]
+    nch, f = int(N["n_children"]), int(N["first_edge"])
+    if nch == 0:
+        return np.zeros(0), np.zeros(0), np.zeros(0)
+    if N["flags"] & 1:
+        W = edges[f + 10:f + 40].view(WIDE_DT)[:nch]
+        return W["R"].T.copy(), W["S"].T.copy(), W["CS"].T.copy()
+    E = edges[f:f + nch]
+    return E["R"].copy(), E["S"].copy(), E["CS"].copy()
 
 
 class HostCfr:
@@ -112,21 +126,22 @@ class HostCfr:
                                   C.c_int(hi), _p(steps))
         return steps
 
-    def decide(self, iters):
+    def decide(self, iters, flags=0):
         hb = self.hb
         chosen = np.zeros((hb.B, 16), np.uint8)
         stats = np.zeros((hb.B, 5), np.int32)
         lib().cith_cfr_decide(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(self.npmt), _p(self.npidx), _p(hb.seer),
-                              C.c_int(hb.B), C.c_int(iters), _p(self.pool), C.c_int(self.node_cap),
+                              C.c_int(hb.B), C.c_int(iters), C.c_int(flags), _p(self.pool), C.c_int(self.node_cap),
                               C.c_int(self.edge_cap), _p(self.optbuf), _p(chosen), _p(stats))
         return chosen, stats
 
     def tree(self, l):
         per = cfr_pool_bytes(self.node_cap, self.edge_cap)
         base = self.pool[l * per:(l + 1) * per]
-        nodes = base[:self.node_cap * 168].view(NODE_DT)
-        edges = base[self.node_cap * 168:self.node_cap * 168 + self.edge_cap * 168].view(EDGE_DT)
-        rows = base[self.node_cap * 168 + self.edge_cap * 168:].reshape(self.node_cap, L.GAME_BYTES)
+        nb, eb = self.node_cap * 168, self.edge_cap * 48
+        nodes = base[:nb].view(NODE_DT)
+        edges = base[nb:nb + eb].view(EDGE_DT)
+        rows = base[nb + eb:].reshape(self.node_cap, L.GAME_BYTES)
         return nodes, edges, rows
 
 

@@ -32,13 +32,25 @@ def test_layout_matches(lib):
     assert list(out[:n]) == L.expected_layout()
     assert lib.cit_game_bytes() == L.GAME_BYTES
     assert lib.cit_seer_scratch_words() == L.SEER_MAX
-    assert lib.cit_abi_version() == 1
+    assert lib.cit_abi_version() == 2
+
+
+def test_cfr_pool_bytes_64bit(lib):
+    # cfr_train(200000) pools exceed 2 GiB per tree (round 1 returned -1 there)
+    nc, ec = 500_256, 5 * 500_256
+    assert lib.cit_cfr_pool_bytes(nc, ec) == nc * 168 + ec * 48 + nc * L.GAME_BYTES
+    assert lib.cit_cfr_pool_bytes(4_000_000, 20_000_000) > 2 ** 31
+    assert lib.cit_cfr_pool_bytes(0, 10) == -1
 
 
 def test_bad_args_rejected(lib):
     # argument validation happens before any launch: no GPU is touched
     assert lib.cit_rollout_random(None, None, None, None, 0, -1, 0, None, None, None) == -1
     assert lib.cit_init(None, None, None, 4, None, 1, None) == -1
+    assert lib.cit_count_options(None, None, None, None, 4, None, None) == -1
+    assert lib.cit_determinize(None, None, None, 4, None, 1, None) == -1
+    assert lib.cit_skip_false_choice(None, None, None, None, 4, None, None) == -1
+    assert lib.cit_cfr_action_choice(None, 4, 16, 16, None, None, None, None, None, None) == -1
 
 
 def test_api_error_mapping():

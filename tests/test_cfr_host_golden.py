@@ -15,7 +15,7 @@ import pytest
 from citadels_self_play_amd import canon
 from citadels_self_play_amd import layout as L
 from conftest import load_golden
-from hostcheck import HostBatch, HostCfr
+from hostcheck import HostBatch, HostCfr, node_arrays
 
 RTOL = 1e-12
 
@@ -25,14 +25,8 @@ def hash_obj(d):
 
 
 def arrays(nodes, edges, i):
-    n = nodes[i]
-    nch = int(n["n_children"])
-    if nch == 0 and n["first_edge"] < 0:
-        return [], [], []
-    E = edges[n["first_edge"]:n["first_edge"] + nch]
-    if n["flags"] & 1:
-        return E["R"].T.tolist(), E["S"].T.tolist(), E["CS"].T.tolist()
-    return E["R"][:, 0].tolist(), E["S"][:, 0].tolist(), E["CS"][:, 0].tolist()
+    R, S, CS = node_arrays(nodes, edges, i)
+    return R.tolist(), S.tolist(), CS.tolist()
 
 
 def dfs(nodes, edges, i, out):

@@ -104,3 +104,45 @@ def test_api_setup_game_matches_reference():
         done += 1
         if done == 4:
             break
+
+
+def test_api_cfrnode_constructor_skip_and_live_false_sampler():
+    """CFRNode(game) runs skip_false_choice on `game` in the constructor
+    (deep_mccfr.py:19-20); after run_mccfr's search, action_choice(live=False)
+    draws children with the in-search sampler from the tree's numpy stream
+    (:67-91) -- both against the oracle's Tree / Node.choose."""
+    import cfr_oracle as CO
+    st = api.default_stream()
+    done = 0
+    for seed in range(300, 340):
+        pos = CO.config3_position(seed)
+        if pos is None:
+            continue
+        og, npr = pos
+        st.seed(seed)
+        g = api.create_game()
+        k = st.randint(0, 300)
+        for _ in range(k):
+            options = g.get_options_from_state()
+            if options[st.randint(0, len(options) - 1)].carry_out(g):
+                break
+        assert canon.canon_game(g.packed()) == O.canon(og), seed
+        node = api.CFRNode(g, g.gamestate.player_id)
+        og.nprng = npr
+        tr = CO.Tree(og, og.gs.pid, np_rng=npr)          # its root Node runs skip_forced on og
+        assert canon.canon_game(g.packed()) == O.canon(og), seed
+        node.cfr_train(max_iterations=200)
+        tr.cfr_train(200)
+        assert node.node_count == tr.count and node.carry_outs == tr.carry_outs, seed
+        _, chosen = node.action_choice(live=True)
+        _, ochosen = tr.root.choose(live=True)
+        assert chosen.name == ochosen.name, seed
+        for _ in range(3):
+            child, opt = node.action_choice(live=False)
+            ochild, oopt = tr.root.choose(live=False)
+            assert opt.name == oopt.name, seed
+            assert child.node_value.tolist() == np.asarray(ochild.nv, float).tolist(), seed
+        done += 1
+        if done == 6:
+            break
+    assert done == 6

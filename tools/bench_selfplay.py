@@ -11,9 +11,10 @@ per GPU (run under torchrun for N > 1; 1 GPU otherwise):
 
 Timed region: barrier + synchronize on both sides, max over ranks; inputs
 (positions) are built before it except for config 5, whose position
-generation is part of simulate_game.  Prints one JSON line (rank 0) with
-decisions/s (or trees/s), carry_out transitions/s inside the searches and
-the per-kernel HIP-event times.
+generation is part of simulate_game.  One untimed-for-the-summary warm-up
+rep, then --reps timed reps; prints one JSON line (rank 0) with the MEDIAN
+rep (decisions/s or trees/s, carry_out transitions/s inside the searches)
+and every rep.
 """
 import argparse
 import json
@@ -36,16 +37,17 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per GPU")
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--node-cap", type=int, default=None)
-    ap.add_argument("--edge-cap", type=int, default=None, help="default 8 x node cap (config 5: 2.5 x)")
-    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--edge-cap", type=int, default=None, help="default engine.pool_caps(iters)")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seed", type=int, default=30_000_000)
     a = ap.parse_args()
     rank, world, dev = selfplay.init_distributed()
-    # config 5: 1024 trees per GPU (one wave per SIMD); a 20000-step tree peaks at
-    # ~83 k nodes / 190 k edges, so the default pool (5 x iters nodes, 2.5 x as
-    # many edges: 219 GB per GPU at 1024 trees) avoids overflow re-searches
-    B = a.batch or {3: 1024, 4: 4096 // max(1, world) if world > 1 else 4096, 5: 1024}[a.config]
+    # config 5: 1024 trees per GPU at 20000 iterations (one wave per SIMD), 64 at
+    # the reference's 200000 (engine.pool_caps sizes the pools; ~1 GB per tree)
     iters = a.iters or {3: 200, 4: 200, 5: 20000}[a.config]
+    B = a.batch or {3: 1024, 4: 4096 // max(1, world) if world > 1 else 4096,
+                    5: 1024 if iters <= 20000 else 64}[a.config]
     net = None
     if a.config == 4:
         from citadels_self_play_amd import models
@@ -53,7 +55,7 @@ def main():
         m = selfplay.broadcast_model(models.ValueOnlyNN(418, 512).to(dev).eval())
         net = models.ValueNet(m, dev)
     out = []
-    for rep in range(a.reps):
+    for rep in range(a.warmup + a.reps):
         seeds = selfplay.shard(B * world, base_seed=a.seed + rep * B * world)
         b = None
         if a.config in (3, 4):
@@ -71,17 +73,19 @@ def main():
         elif a.config == 4:
             chosen, stats, rounds = b.cfr_pred(iters, net, max_depth=10, node_cap=a.node_cap or 2048)
         else:
-            nc = a.node_cap or max(1024, 5 * iters)
-            b, stats, t = selfplay.simulate_games(seeds, iters, node_cap=nc, edge_cap=a.edge_cap or 5 * nc // 2)
+            b, stats, t = selfplay.simulate_games(seeds, iters, node_cap=a.node_cap, edge_cap=a.edge_cap,
+                                                  log=(lambda m: print(m, file=sys.stderr, flush=True)))
             f, v = selfplay.all_gather_targets(t["feat"], t["value"])
             n_targets = int(f.shape[0])
-            term = b.terminal()            # k = 1 picks the final (terminal) game: ValueError in the reference
+            # k = 1 picks the final (terminal) game: ValueError in the reference (known only for one chunk)
+            term = b.terminal() if b.B == stats.shape[0] else torch.zeros(stats.shape[0], dtype=torch.bool,
+                                                                            device=dev)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
         st = stats.to(dev).to(torch.float64)
-        tot = torch.tensor([el, float(b.B), float(st[:, 3].sum()), float(((st[:, 4] != 0) & ~term).sum()),
+        tot = torch.tensor([el, float(st.shape[0]), float(st[:, 3].sum()), float(((st[:, 4] != 0) & ~term).sum()),
                             float(term.sum()), float(st[:, 1].sum()), float(st[:, 1].max()), float(st[:, 2].max())],
                            dtype=torch.float64,
                            device=dev)
@@ -91,14 +95,18 @@ def main():
             dist.all_reduce(tot)
             tot[0], tot[6], tot[7] = tmax[0], tmax[6], tmax[7]
         el, units, carry, errs, terms, nodes, nodes_max, edges_max = [float(x) for x in tot]
+        if rank == 0:
+            print("rep %d: %.2fs" % (rep, el), file=sys.stderr, flush=True)
         out.append({"config": a.config, "n_gpus": world, "per_gpu": B, "iters": iters, "seconds": el,
+                    "warmup": rep < a.warmup,
                     ("trees_per_s" if a.config == 5 else "decisions_per_s"): units / el,
                     "carry_out_per_s": carry / el, "nodes_mean": nodes / units, "nodes_max": int(nodes_max), "edges_max": int(edges_max), "rounds": rounds,
                     "pooled_targets": n_targets, "error_lanes_nonterminal": int(errs),
                     "terminal_positions": int(terms)})
     if rank == 0:
-        best = max(out, key=lambda r: r["carry_out_per_s"])
-        print(json.dumps({"best": best, "reps": out}), flush=True)
+        timed = sorted([r for r in out if not r["warmup"]], key=lambda r: r["carry_out_per_s"])
+        median = timed[len(timed) // 2] if timed else None
+        print(json.dumps({"median": median, "reps": out}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

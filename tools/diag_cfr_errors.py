@@ -24,6 +24,13 @@ def report(tag, seeds, b, stats):
 
 def main():
     torch.cuda.set_device(0)
+    if len(sys.argv) > 2:                 # diag_cfr_errors.py ITERS TREES
+        iters, n = int(sys.argv[1]), int(sys.argv[2])
+        seeds = selfplay.shard(n, base_seed=30_000_000)
+        b, stats, _ = selfplay.simulate_games(seeds, iters)
+        torch.cuda.synchronize()
+        report("config5_%d" % iters, seeds, b, stats)
+        return
     seeds = selfplay.shard(1024, base_seed=30_000_000)
     b, stats, _ = selfplay.simulate_games(seeds, 2000)
     torch.cuda.synchronize()

@@ -40,6 +40,7 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   __shared__ __attribute__((aligned(16))) CitOpt lbufs[CFR_LBUF];
   long l = blockIdx.x;
   if (l >= B) return;
+  cfr_prof_reset();
   __shared__ CfrTree T;     // shared: the wavefront's lanes update it in lockstep
   cfr_tree_bind(T, pool, l, node_cap, edge_cap);
   T.n_nodes = T.n_edges = 0;
@@ -73,6 +74,7 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
     stats[5 * l + 3] = (int)T.carry_outs;
     stats[5 * l + 4] = (int)T.err;
   }
+  cfr_prof_flush();
 }
 
 // One resumption of cfr_pred (cit_cfr.h: cfr_pred_run) per tree; lane 0 adds

@@ -43,12 +43,12 @@ def node_arrays(nodes, edges, n):
 
 
 def pool_caps(iters):
-    """Node / edge capacity for a cfr_train(iters) tree: measured 1.8-2.3
-    nodes and 3.5-4.4 reserved edge slots per node at 2k-200k iterations
-    (tools/cfr_tree_sizes.py); a tree that still outgrows its pool is searched
-    again with a 4x pool (GameBatch._retry_overflow)."""
-    node_cap = max(1024, int(2.5 * iters) + 256)
-    return node_cap, 5 * node_cap
+    """Node / edge capacity for a cfr_train(iters) tree: measured 1.2-3.3 nodes
+    per iteration (2000 iterations: up to 6,604 nodes; 200000: up to 646,897)
+    and 3.1-4.4 reserved edge slots per node; a tree that still outgrows its
+    pool is searched again with a 4x pool (GameBatch._retry_overflow)."""
+    node_cap = max(1024, int(3.5 * iters) + 512)
+    return node_cap, 4 * node_cap + 4096
 
 
 def _ptr(t):
@@ -379,7 +379,13 @@ class GameBatch:
         return chosen, stats, rounds
 
     def tree(self, lane):
-        """(nodes, edges, rows) numpy views of one lane's search tree (host copy)."""
+        """(nodes, edges, rows) numpy views of one lane's search tree (host copy);
+        a lane searched again after a pool overflow is read from its retry batch."""
+        retry = getattr(self, "_retry", None)
+        if retry is not None:
+            over = retry[0].cpu().tolist()
+            if lane in over:
+                return retry[1].tree(over.index(lane))
         per = self.lib.cit_cfr_pool_bytes(self.node_cap, self.edge_cap)
         base = self.pool[lane * per:(lane + 1) * per].cpu().numpy()
         nb, eb = self.node_cap * NODE_DT.itemsize, self.edge_cap * EDGE_DT.itemsize

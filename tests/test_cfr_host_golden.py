@@ -60,7 +60,7 @@ def compare_node(nodes, edges, rows, i, want, where):
 def run_cases(recs):
     recs = [r for r in recs if not r.get("skip")]
     hb = HostBatch([r["seed"] for r in recs], True)
-    cf = HostCfr(hb, node_cap=6144, edge_cap=8 * 6144)
+    cf = HostCfr(hb, node_cap=8192, edge_cap=5 * 8192)
     cf.advance(0, 300)
     for l, r in enumerate(recs):
         assert canon.canon_game(hb.game(l)) == r["position"], r["seed"]

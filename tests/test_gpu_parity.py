@@ -198,3 +198,22 @@ def test_gpu_rollout_u_option_overflow(engine):
         assert wa[l] == og.winner, l
         assert canon.canon_game(L.game_from_bytes(rows_a[l])) == O.canon(og), l
     assert big_draws >= 50, big_draws
+
+
+@pytest.mark.parametrize("preset", [True, False])
+def test_gpu_fingerprint_matches_reference(engine, preset):
+    """SURVEY §6 fingerprint of the reference's own random-policy games
+    (tests/golden/fingerprint.json.gz, tools/gen_golden.py): seeds 0..399 preset /
+    0..199 random-role through k_rollout_u -- seat win counts, total steps and
+    total winner points exact."""
+    from conftest import load_golden
+    fp = [f for f in load_golden("fingerprint.json.gz") if f["preset"] == preset][0]
+    b = engine(list(range(fp["games"])), preset=preset)
+    steps, w = b.rollout(games_per_block=0)
+    steps, w = steps.cpu().numpy(), w.cpu().numpy()
+    assert int((b.errors() != 0).sum()) == fp["errors"] == 0
+    assert np.bincount(w, minlength=6).tolist() == fp["wins"]
+    assert int(steps.sum()) == fp["steps"]
+    off = L.CitGame.points.offset
+    pts = b.rows()[:, off:off + 12].copy().view(np.int16).reshape(-1, 6)
+    assert int(pts.max(axis=1).sum()) == fp["winner_points"]

@@ -23,16 +23,21 @@ def _split(t):
     return per
 
 
-def test_gpu_targets_golden():
-    from citadels_self_play_amd.engine import GameBatch
-    recs = load_golden("targets2000.json.gz")
+@pytest.mark.parametrize("name,iters", [("targets2000.json.gz", 2000), ("targets20000.json.gz", 20000)])
+def test_gpu_targets_golden(name, iters):
+    """simulate_game trees of the reference (cfr_train(2000), 16 seeds; and the
+    config-5 quick setting cfr_train(20000), 4 seeds): positions, node and
+    carry_out counts, decisions, both streams' end states, every target."""
+    from citadels_self_play_amd.engine import GameBatch, pool_caps
+    recs = [r for r in load_golden(name) if not r.get("error")]
     b = GameBatch([r["seed"] for r in recs], preset=True)
     b.random_position(100)
     rows = b.rows()
     for l, r in enumerate(recs):
         assert canon.canon_game(L.game_from_bytes(rows[l])) == r["position"], r["seed"]
     b.seed_numpy()
-    chosen, stats = b.cfr_decide(2000, node_cap=8192)
+    nc, ec = pool_caps(iters)
+    chosen, stats = b.cfr_decide(iters, node_cap=nc, edge_cap=ec)
     per = _split(b.cfr_targets(stats[:, 0]))
     chosen, stats, rows = chosen.cpu().numpy(), stats.cpu().numpy(), b.rows()
     mt = b.mt.cpu().numpy().view(np.uint32)

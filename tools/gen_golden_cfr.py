@@ -144,8 +144,21 @@ def main_pred():
         json.dump(recs, f, separators=(",", ":"))
 
 
+def main_2000():
+    """cfr_train2000.json.gz: 16 seeds, root records, no trees."""
+    recs = []
+    t = time.time()
+    for s in range(100, 116):
+        recs.append(case(s, 2000, tree=False))
+        print(s, recs[-1].get("nodes"), recs[-1].get("carry_outs"), "%.1fs" % (time.time() - t), flush=True)
+    with gzip.open(os.path.join(OUT, "cfr_train2000.json.gz"), "wt") as f:
+        json.dump(recs, f, separators=(",", ":"))
+
+
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "pred":
     main_pred()
+elif __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "2000":
+    main_2000()
 elif __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     recs = []

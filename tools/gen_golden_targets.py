@@ -75,12 +75,16 @@ def case(seed, iters):
 
 
 def main():
+    """python tools/gen_golden_targets.py [ITERS N_SEEDS]: targets2000.json.gz (16
+    seeds) by default; targets20000.json.gz = cfr_train(20000), 4 seeds."""
     os.makedirs(OUT, exist_ok=True)
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     recs = []
-    for s in range(16):
-        recs.append(case(s, 2000))
+    for s in range(n):
+        recs.append(case(s, iters))
         print(s, recs[-1].get("error"), recs[-1].get("nodes"), len(recs[-1].get("targets", [])), flush=True)
-    with gzip.open(os.path.join(OUT, "targets2000.json.gz"), "wt") as f:
+    with gzip.open(os.path.join(OUT, "targets%d.json.gz" % iters), "wt") as f:
         json.dump(recs, f, separators=(",", ":"))
 
 

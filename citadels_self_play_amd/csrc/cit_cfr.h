@@ -100,14 +100,18 @@ CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, long l, int node_cap, int e
   T.node_cap = node_cap;
   T.edge_cap = edge_cap;
 }
-// the [6]-wide regret / strategy columns of role-pick child a
-CIT_HD CfrWide* cfr_wide(const CfrTree& T, int first_edge) {
-  return reinterpret_cast<CfrWide*>(T.edges + first_edge + CFR_ROLE_CHILDREN);
-}
+// Resumable cfr_pred state of one tree (see cfr_pred_run below): 64 B,
+// persists in HBM between launches.
+enum { CP_INIT = 0, CP_RUN = 1, CP_WAIT = 2, CP_DONE = 3 };
+struct CfrState {
+  int32_t n_nodes, n_edges, err, carry_outs;
+  int32_t cur, it, phase, pending;
+  int32_t root, orig, pad[6];
+};
+static_assert(sizeof(CfrState) == 64, "CfrState layout");
 
 // The 64 lanes of a tree's workgroup (one wavefront) run the search in
-// lockstep on shared state (the CfrTree itself lives in LDS); row copies are
-// split across them.
+// lockstep on shared state; row copies are split across them.
 #if defined(__HIP_DEVICE_COMPILE__)
 #define CFR_SYNC() __syncthreads()
 #define CFR_LANE ((int)threadIdx.x)
@@ -118,28 +122,89 @@ CIT_HD CfrWide* cfr_wide(const CfrTree& T, int first_edge) {
 #define CFR_TEAM 1
 #endif
 
-// The search's working state (the CfrTree, the two MT19937 streams, the
-// working rows w0/w1, the determinization scratch) lives in LDS, but the
-// out-of-line functions below receive it through generic references, which
-// the compiler addresses with flat instructions.  cfr_lds() re-derives such a
-// reference through an LDS pointer, so everything inlined below it uses ds_*
-// instructions.  Only for CIT_WAVE units (the search kernels); the
-// one-tree-per-lane target kernels and the host build keep plain references.
+// ------------------------------------------------ uniformity, address spaces
+// Every lane of a search team holds the same values, but a value that crosses
+// a call boundary (an argument, a return value) arrives in a VGPR, and the
+// compiler then treats everything derived from it as divergent: vector ALU
+// for scalar work, exec-masked branches, and flat memory instructions (which
+// wait on both the LDS and the vector-memory counters).  The search therefore
+// (1) keeps its working state in one namespace-scope LDS block (cfr_ls, fixed
+// addresses), (2) re-uniformises arguments and returns with readfirstlane
+// (cfr_u) and (3) reaches the HBM node pool through pointers cast to the
+// global address space (cfr_glb: global_* instructions with scalar bases).
 #if CIT_WAVE
+#define CFR_GAS __attribute__((address_space(1)))
+__device__ __forceinline__ int cfr_u(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t cfr_u(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 template <class X>
-__device__ __forceinline__ X& cfr_lds(X& x) {
-  __builtin_assume(__builtin_amdgcn_is_shared((const void*)&x));
-  return x;
+__device__ __forceinline__ X* cfr_glb(X* q) {
+  uint64_t a = (uint64_t)(uintptr_t)q;
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  return (X*)(CFR_GAS X*)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ CitOpt cfr_uopt(const CitOpt& o) {
+  uint32_t w[4];
+  __builtin_memcpy(w, &o, 16);
+  for (int i = 0; i < 4; i++) w[i] = cfr_u(w[i]);
+  CitOpt r;
+  __builtin_memcpy(&r, w, 16);
+  return r;
 }
 #else
+CIT_HD int cfr_u(int v) { return v; }
+CIT_HD uint32_t cfr_u(uint32_t v) { return v; }
 template <class X>
-CIT_HD X& cfr_lds(X& x) { return x; }
+CIT_HD X* cfr_glb(X* p) { return p; }
+CIT_HD CitOpt cfr_uopt(const CitOpt& o) { return o; }
 #endif
+
+// The search's working state.  Device (CIT_WAVE): one LDS block per
+// workgroup at namespace scope (the tree, the resumable pred state, the two
+// working rows w0 / w1, the two MT19937 streams, the option list buffer and
+// the determinization scratch); the CfrTree / CfrState references the
+// functions receive are then only the host build's.  Host: the pointers
+// bound in CfrTree.
+#if defined(__HIPCC__)
+struct CfrLds {
+  CfrTree T;
+  CfrState S;
+  uint32_t w[2][CIT_GAME_BYTES / 4];
+  uint32_t py[CIT_MT_N], np[CIT_MT_N];
+  CitOpt lbuf[CFR_LBUF];
+  uint8_t tmp[128];
+};
+static __shared__ __attribute__((aligned(16))) CfrLds cfr_ls;
+#endif
+#if CIT_WAVE
+#define CFR_T(T_in) (cfr_ls.T)
+#define CFR_S(S_in) (cfr_ls.S)
+__device__ __forceinline__ CitGame& cfr_w(const CfrTree&, int which) {
+  return *reinterpret_cast<CitGame*>(cfr_ls.w[which]);
+}
+__device__ __forceinline__ CitOpt* cfr_lbuf(const CfrTree&) { return cfr_ls.lbuf; }
+__device__ __forceinline__ uint8_t* cfr_tmp(const CfrTree&) { return cfr_ls.tmp; }
+#else
+#define CFR_T(T_in) (T_in)
+#define CFR_S(S_in) (S_in)
+CIT_HD CitGame& cfr_w(const CfrTree& T, int which) { return which ? *T.w1 : *T.w0; }
+CIT_HD CitOpt* cfr_lbuf(const CfrTree& T) { return T.lbuf; }
+CIT_HD uint8_t* cfr_tmp(const CfrTree& T) { return T.tmp; }
+#endif
+CIT_HD CfrNode* cfr_nd(const CfrTree& T) { return cfr_glb(T.nodes); }
+CIT_HD CfrEdge* cfr_ed(const CfrTree& T) { return cfr_glb(T.edges); }
+// the [6]-wide regret / strategy columns of role-pick child a
+CIT_HD CfrWide* cfr_wide(const CfrTree& T, int first_edge) {
+  return reinterpret_cast<CfrWide*>(cfr_ed(T) + first_edge + CFR_ROLE_CHILDREN);
+}
+CIT_HD uint32_t* row_of(const CfrTree& T, int id) { return cfr_glb(T.rows) + (long)id * (CIT_GAME_BYTES / 4); }
+CIT_HD uint32_t* w_row(const CfrTree& T, int which) { return reinterpret_cast<uint32_t*>(&cfr_w(T, which)); }
 
 // One out-of-line copy of each engine entry point for the search: the
 // engine is force-inlined by default (the rollout kernel wants that), and
 // inlining it at every call site of the search multiplies code size and
-// compile time.  The search reaches LDS rows through flat pointers here.
+// compile time.  Arguments are small values (a working-row selector, an
+// option, an index); the state is reached through cfr_ls.
 #if defined(__HIPCC__)
 #define CIT_NOINLINE __host__ __device__ inline __attribute__((noinline))
 #else
@@ -183,41 +248,60 @@ __device__ inline void cfr_prof_flush() {
 #define cfr_prof_reset() ((void)0)
 #define cfr_prof_flush() ((void)0)
 #endif
-CIT_NOINLINE int eng_carry(CitGame& g, const CitOpt& o, CitMT& r) {
-  CIT_PROF_SCOPE(0); return cit_carry_out(cfr_lds(g), o, cfr_lds(r)); }
-CIT_NOINLINE void eng_prepare(CitGame& g, CitMT& r, uint64_t* seer) {
-  CIT_PROF_SCOPE(1); cit_prepare_options(cfr_lds(g), cfr_lds(r), seer); }
-CIT_NOINLINE int eng_count(const CitGame& g, uint32_t& err, const uint64_t* seer) {
-  CIT_PROF_SCOPE(2);
-  return cit_count_options(cfr_lds(g), err, seer);
+
+// option.carry_out on working row `which`, counted; returns the winner (-1: none)
+CIT_NOINLINE int eng_carry(CfrTree& T_in, int which, CitOpt o_in) {
+  CIT_PROF_SCOPE(0);
+  CfrTree& T = CFR_T(T_in);
+  CitOpt o = cfr_uopt(o_in);
+  T.carry_outs++;
+  return cit_carry_out(cfr_w(T, cfr_u(which)), o, T.py);
 }
-CIT_NOINLINE CitOpt eng_pick(const CitGame& g, int k, const uint64_t* seer) {
-  CIT_PROF_SCOPE(3); return cit_pick_option(cfr_lds(g), k, seer); }
-CIT_NOINLINE int eng_list(const CitGame& g, CitOpt* buf, int cap, uint32_t& err, const uint64_t* seer) {
+CIT_NOINLINE void eng_prepare(CfrTree& T_in, int which) {
+  CIT_PROF_SCOPE(1);
+  CfrTree& T = CFR_T(T_in);
+  cit_prepare_options(cfr_w(T, cfr_u(which)), T.py, cfr_glb(T.seer));
+}
+CIT_NOINLINE CitOpt eng_pick(CfrTree& T_in, int which, int k) {
+  CIT_PROF_SCOPE(3);
+  CfrTree& T = CFR_T(T_in);
+  return cit_pick_option(cfr_w(T, cfr_u(which)), cfr_u(k), cfr_glb(T.seer));
+}
+// An option count and the enumeration's error bits (returned, not written
+// through a pointer: an out-parameter of a call lives in scratch memory).
+struct CfrCnt {
+  int n;
+  uint32_t err;
+};
+CIT_HD CfrCnt cfr_ucnt(CfrCnt c) { return {cfr_u(c.n), cfr_u(c.err)}; }
+// Every option of working row `which` into T.optbuf (HBM, CFR_OPT_CAP).
+CIT_NOINLINE CfrCnt eng_list(CfrTree& T_in, int which) {
   CIT_PROF_SCOPE(4);
-  ListSink s(buf, cap);
-  cit_enum_options(cfr_lds(g), s, seer);
-  err |= s.err;
-  return s.n;
+  CfrTree& T = CFR_T(T_in);
+  ListSink s(cfr_glb(T.optbuf), CFR_OPT_CAP);
+  cit_enum_options(cfr_w(T, cfr_u(which)), s, cfr_glb(T.seer));
+  return {s.n, s.err};
 }
-// A search step's option list: the first CFR_LBUF options land in T.lbuf (LDS)
-// while all are counted, so one enumeration serves both the count and the
-// draw (opt_at re-enumerates only for an index past the buffer).
-CIT_NOINLINE int eng_list_lds(const CitGame& g, CitOpt* lbuf, uint32_t& err, const uint64_t* seer) {
+// A search step's option list: the first CFR_LBUF options land in the LDS
+// list buffer while all are counted, so one enumeration serves both the count
+// and the draw (eng_pick re-enumerates only for an index past the buffer).
+CIT_NOINLINE CfrCnt eng_list_lds(CfrTree& T_in, int which) {
   CIT_PROF_SCOPE(2);
-  ListSink s(&cfr_lds(*lbuf), CFR_LBUF);
-  cit_enum_options(cfr_lds(g), s, seer);
-  err |= s.err;
-  return s.n;
+  CfrTree& T = CFR_T(T_in);
+  ListSink s(cfr_lbuf(T), CFR_LBUF);
+  cit_enum_options(cfr_w(T, cfr_u(which)), s, cfr_glb(T.seer));
+  return {s.n, s.err};
 }
-CIT_NOINLINE void eng_sample(CitGame& g, int orig, bool role_sample, CitMT& r, uint8_t* unk) {
+CIT_NOINLINE void eng_sample(CfrTree& T_in, int which, int orig, int role_sample) {
   CIT_PROF_SCOPE(5);
-  cit_sample_private(cfr_lds(g), orig, role_sample, cfr_lds(r), &cfr_lds(*unk));
+  CfrTree& T = CFR_T(T_in);
+  cit_sample_private(cfr_w(T, cfr_u(which)), cfr_u(orig), cfr_u(role_sample) != 0, T.py, cfr_tmp(T));
 }
 
-CIT_HD uint32_t* row_of(const CfrTree& T, int id) { return T.rows + (long)id * (CIT_GAME_BYTES / 4); }
-// deepcopy(game): the team copies one row
-CIT_NOINLINE void copy_row(const CfrTree& T, uint32_t* dst, const uint32_t* src) {
+// deepcopy(game): the team copies one row (inlined, so each call site's
+// source and destination address spaces are known)
+CIT_HD void copy_row(const CfrTree& T, uint32_t* dst, const uint32_t* src) {
+  (void)T;
   CIT_PROF_SCOPE(6);
   CFR_SYNC();
   for (int i = CFR_LANE; i < CIT_GAME_BYTES / 4; i += CFR_TEAM) dst[i] = src[i];
@@ -364,41 +448,42 @@ CIT_HD void opt_mutate(CitOpt& o, const CitGame& g) {
 }
 
 // -------------------------------------------------------------- nodes
-CIT_NOINLINE void tree_carry(CfrTree& T_in, CitGame& g, const CitOpt& o, int& winner) {
-  CfrTree& T = cfr_lds(T_in);
-  winner = eng_carry(g, o, T.py);
-  T.carry_outs++;
-}
-
-// CFRNode(game=w, parent, depth): skip_false_choice on w, then a new node
-// whose row is w.  `skipped`: the caller already ran skip_false_choice on w
-// (the facade's CFRNode constructor), so it is not run again.  Returns the
-// node id (-1 on error).
-CIT_NOINLINE int cfr_node(CfrTree& T_in, CitGame& w, int parent, int depth, bool skipped = false) {
-  CfrTree& T = cfr_lds(T_in);
+// CFRNode(game=w, parent, depth): skip_false_choice on working row `which`,
+// then a new node whose row is that game.  `skipped`: the caller already ran
+// skip_false_choice (the facade's CFRNode constructor), so it is not run
+// again.  Returns the node id (-1 on error).
+CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int skipped) {
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(7);
+  which = cfr_u(which);
+  parent = cfr_u(parent);
+  depth = cfr_u(depth);
+  CitGame& w = cfr_w(T, which);
   uint32_t e = 0;
   int n = 0;
-  if (!skipped) {
-    eng_prepare(w, T.py, T.seer);
-    n = eng_list_lds(w, T.lbuf, e, T.seer);
+  if (!cfr_u(skipped)) {
+    eng_prepare(T, which);
+    CfrCnt c = cfr_ucnt(eng_list_lds(T, which));
+    n = c.n;
+    e |= c.err;
   }
   int i = 0;
   bool done = false;
   while (n == 1 && !done && !e && !w.err) {
     i++;
-    CitOpt o = T.lbuf[0];
-    int win;
-    tree_carry(T, w, o, win);
+    CitOpt o = cfr_lbuf(T)[0];
+    int win = cfr_u(eng_carry(T, which, o));
     done = win >= 0;
-    eng_prepare(w, T.py, T.seer);
-    n = eng_list_lds(w, T.lbuf, e, T.seer);
+    eng_prepare(T, which);
+    CfrCnt c = cfr_ucnt(eng_list_lds(T, which));
+    n = c.n;
+    e |= c.err;
     if (i > 100) done = true;
   }
   T.err |= e | w.err;
   if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
   int id = T.n_nodes++;
-  CfrNode& N = T.nodes[id];
+  CfrNode& N = cfr_nd(T)[id];
   N.parent = parent;
   N.first_edge = -1;
   N.n_children = 0;
@@ -409,7 +494,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, CitGame& w, int parent, int depth, bool
   N.flags = (uint8_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0));
   N.winner = w.winner;
   for (int k = 0; k < 6; k++) N.nv[k] = N.wp[k] = N.pred[k] = 0.0;
-  copy_row(T, row_of(T, id), reinterpret_cast<const uint32_t*>(&w));
+  copy_row(T, row_of(T, id), w_row(T, which));
   return id;
 }
 
@@ -427,119 +512,123 @@ CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
 
 // ------------------------------------------------------------ expansion
 CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
-  CfrTree& T = cfr_lds(T_in);
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(8);            // :102-131
+  n = cfr_u(n);
+  CfrNode* ND = cfr_nd(T);
+  CfrEdge* ED = cfr_ed(T);
   int f = alloc_edges(T, CFR_ROLE_EDGE_SLOTS);
   if (f < 0) return;
   CfrWide* W = cfr_wide(T, f);
   for (int r = 0; r < CFR_ROLE_CHILDREN; r++)
     for (int k = 0; k < 6; k++) W[r].R[k] = W[r].S[k] = W[r].CS[k] = 0.0;
-  T.nodes[n].first_edge = f;
-  T.nodes[n].edge_cap = CFR_ROLE_CHILDREN;
-  int depth = T.nodes[n].depth + 1;
+  ND[n].first_edge = f;
+  ND[n].edge_cap = CFR_ROLE_CHILDREN;
+  int depth = ND[n].depth + 1;
+  CitGame& h = cfr_w(T, 1);
   for (int r = 0; r < CFR_ROLE_CHILDREN && !T.err; r++) {
-    copy_row(T, reinterpret_cast<uint32_t*>(T.w1), row_of(T, n));
-    CitGame& h = *T.w1;
+    copy_row(T, w_row(T, 1), row_of(T, n));
     CitOpt last = mk(O_NUM_NAMES, 0);
     int guard = 0;
     while (h.gs_state != 1 && !T.err) {
-      uint32_t e = 0;
-      eng_prepare(h, T.py, T.seer);
-      int cnt = eng_list_lds(h, T.lbuf, e, T.seer);
-      T.err |= e;
-      int k = np_choice_uniform(T.np, cnt, T.err);
+      eng_prepare(T, 1);
+      CfrCnt c = cfr_ucnt(eng_list_lds(T, 1));
+      T.err |= c.err;
+      int k = np_choice_uniform(T.np, c.n, T.err);
       if (T.err) break;
-      last = k < CFR_LBUF ? T.lbuf[k] : eng_pick(h, k, T.seer);
-      int win;
-      tree_carry(T, h, last, win);
+      last = k < CFR_LBUF ? cfr_lbuf(T)[k] : cfr_uopt(eng_pick(T, 1, k));
+      eng_carry(T, 1, last);
       T.err |= h.err;
       if (++guard > 64) T.err |= CIT_ERR_UNSUPPORTED;
     }
     if (T.err) return;
-    int c = cfr_node(T, h, n, depth);
+    int c = cfr_u(cfr_node(T, 1, n, depth, 0));
     if (c < 0) return;
-    init_edge(T.edges[f + r], last, c);
-    T.nodes[n].n_children = (int16_t)(r + 1);
+    init_edge(ED[f + r], last, c);
+    ND[n].n_children = (int16_t)(r + 1);
   }
 }
 
 CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
-  CfrTree& T = cfr_lds(T_in);
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(9);                   // :133-151
-  CitGame& g = *T.w0;
-  copy_row(T, reinterpret_cast<uint32_t*>(&g), row_of(T, n));
-  eng_prepare(g, T.py, T.seer);
-  uint32_t le = 0;
-  int nl = eng_list(g, T.optbuf, CFR_OPT_CAP, le, T.seer);
-  T.err |= le | g.err;
+  n = cfr_u(n);
+  CfrNode* ND = cfr_nd(T);
+  CfrEdge* ED = cfr_ed(T);
+  CitGame& g = cfr_w(T, 0);
+  copy_row(T, w_row(T, 0), row_of(T, n));
+  eng_prepare(T, 0);
+  CfrCnt lc = cfr_ucnt(eng_list(T, 0));
+  int nl = lc.n;
+  T.err |= lc.err | g.err;
   if (nl > CFR_OPT_CAP) T.err |= CIT_ERR_OVERFLOW;
-  copy_row(T, row_of(T, n), reinterpret_cast<const uint32_t*>(&g));   // get_options mutated the node's game
+  copy_row(T, row_of(T, n), w_row(T, 0));   // get_options mutated the node's game
   if (T.err) return;
   int cnt = nl;
   int f = alloc_edges(T, cnt);
   if (f < 0) return;
-  CfrNode& N = T.nodes[n];
+  CfrNode& N = ND[n];
   N.first_edge = f;
   N.edge_cap = (int16_t)cnt;
   int par = N.parent;
-  bool sample = par < 0 || N.player != T.nodes[par].player;
-  bool role_sample = par >= 0 && T.nodes[par].gs_state != 0;
+  bool sample = par < 0 || N.player != ND[par].player;
+  bool role_sample = par >= 0 && ND[par].gs_state != 0;
   int depth = N.depth + 1;
+  const CitOpt* ob = cfr_glb(T.optbuf);
+  CitGame& h = cfr_w(T, 1);
   for (int i = 0; i < cnt && !T.err; i++) {
-    CitOpt o = T.optbuf[i];
-    copy_row(T, reinterpret_cast<uint32_t*>(T.w1), reinterpret_cast<const uint32_t*>(&g));
-    CitGame& h = *T.w1;
-    if (sample) eng_sample(h, T.orig, role_sample, T.py, T.tmp);
+    CitOpt o = ob[i];
+    copy_row(T, w_row(T, 1), w_row(T, 0));
+    if (sample) eng_sample(T, 1, T.orig, role_sample);
     opt_mutate(o, h);
-    int win;
-    tree_carry(T, h, o, win);
+    eng_carry(T, 1, o);
     T.err |= h.err;
     if (T.err) return;
-    int c = cfr_node(T, h, n, depth);
+    int c = cfr_u(cfr_node(T, 1, n, depth, 0));
     if (c < 0) return;
-    init_edge(T.edges[f + i], o, c);
-    T.nodes[n].n_children = (int16_t)(i + 1);
+    init_edge(ED[f + i], o, c);
+    ND[n].n_children = (int16_t)(i + 1);
   }
 }
 
 CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
-  CfrTree& T = cfr_lds(T_in);
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(10);              // :153-179
-  CfrNode& N = T.nodes[n];
-  copy_row(T, reinterpret_cast<uint32_t*>(T.w1), row_of(T, n));
-  CitGame& h = *T.w1;
+  n = cfr_u(n);
+  CfrNode* ND = cfr_nd(T);
+  CfrEdge* ED = cfr_ed(T);
+  CfrNode& N = ND[n];
+  copy_row(T, w_row(T, 1), row_of(T, n));
+  CitGame& h = cfr_w(T, 1);
   int par = N.parent;
-  if (par < 0 || N.player != T.nodes[par].player)
-    eng_sample(h, T.orig, par >= 0 && T.nodes[par].gs_state != 0, T.py, T.tmp);
-  uint32_t e = 0;
-  eng_prepare(h, T.py, T.seer);
-  int cnt = eng_list_lds(h, T.lbuf, e, T.seer);
-  T.err |= e | h.err;
-  int k = np_choice_uniform(T.np, cnt, T.err);
+  if (par < 0 || N.player != ND[par].player) eng_sample(T, 1, T.orig, par >= 0 && ND[par].gs_state != 0);
+  eng_prepare(T, 1);
+  CfrCnt lc = cfr_ucnt(eng_list_lds(T, 1));
+  T.err |= lc.err | h.err;
+  int k = np_choice_uniform(T.np, lc.n, T.err);
   if (T.err) return;
-  CitOpt o = k < CFR_LBUF ? T.lbuf[k] : eng_pick(h, k, T.seer);
+  CitOpt o = k < CFR_LBUF ? cfr_lbuf(T)[k] : cfr_uopt(eng_pick(T, 1, k));
   opt_mutate(o, h);
   CitOpt key = opt_key(o, h);
-  int win;
-  tree_carry(T, h, o, win);
+  eng_carry(T, 1, o);
   T.err |= h.err;
   if (T.err) return;
   for (int j = 0; j < N.n_children; j++)
-    if (opt_eq(T.edges[N.first_edge + j].opt, key)) return;
+    if (opt_eq(ED[N.first_edge + j].opt, key)) return;
   if (N.first_edge < 0) {
     int f = alloc_edges(T, CFR_OPP_CHILDREN);
     if (f < 0) return;
     N.first_edge = f;
     N.edge_cap = CFR_OPP_CHILDREN;
   }
-  int c = cfr_node(T, h, n, N.depth + 1);
+  int c = cfr_u(cfr_node(T, 1, n, N.depth + 1, 0));
   if (c < 0) return;
-  init_edge(T.edges[T.nodes[n].first_edge + T.nodes[n].n_children], key, c);
-  T.nodes[n].n_children++;
+  init_edge(ED[ND[n].first_edge + ND[n].n_children], key, c);
+  ND[n].n_children++;
 }
 
 CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
-  CfrNode& N = T.nodes[n];
+  CfrNode& N = cfr_nd(T)[n];
   if (N.gs_state == 0 && N.n_children == 0) {
     N.flags |= NF_ROLE_PICK;
     cfr_expand_role_pick(T, n);
@@ -552,12 +641,13 @@ CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
 
 // ---------------------------------------------------------- strategies
 CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
-  CfrTree& T = cfr_lds(T_in);
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(11);               // :292-319
-  CfrNode& N = T.nodes[n];
+  n = cfr_u(n);
+  CfrNode& N = cfr_nd(T)[n];
   int nch = N.n_children;
   if (nch == 0) return;
-  CfrEdge* E = T.edges + N.first_edge;
+  CfrEdge* E = cfr_ed(T) + N.first_edge;
   if (!(N.flags & NF_ROLE_PICK)) {
     for (int a = 0; a < nch; a++) E[a].S = exp((-E[a].R) * CFR_LN13);
     double tot = np_sum([E](int i) { return E[i].S; }, nch, T.err);
@@ -594,11 +684,12 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
 
 // action_choice(live=False) (:67-91): returns the edge index within the node
 CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
-  CfrTree& T = cfr_lds(T_in);
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(12);
-  CfrNode& N = T.nodes[n];
+  n = cfr_u(n);
+  CfrNode& N = cfr_nd(T)[n];
   int nch = N.n_children;
-  const CfrEdge* E = T.edges + (N.first_edge < 0 ? 0 : N.first_edge);
+  const CfrEdge* E = cfr_ed(T) + (N.first_edge < 0 ? 0 : N.first_edge);
   if (!(N.flags & NF_ROLE_PICK)) {
     double tot = np_sum([E](int i) { return E[i].CS; }, nch, T.err);
     return np_choice(T.np, [E, tot](int i) { return E[i].CS / tot; }, nch, T.err);
@@ -622,23 +713,25 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
 
 // ------------------------------------------------------------- backup
 CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
-  CfrTree& T = cfr_lds(T_in);
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(13);                // :231-256
-  CfrNode& N = T.nodes[n];
-  CfrEdge* E = T.edges + N.first_edge;
+  n = cfr_u(n);
+  CfrNode* ND = cfr_nd(T);
+  CfrNode& N = ND[n];
+  CfrEdge* E = cfr_ed(T) + N.first_edge;
   int nch = N.n_children;
   if (!(N.flags & NF_ROLE_PICK)) {
     int p = N.player;
-    double mx = T.nodes[E[0].child].wp[p];
+    double mx = ND[E[0].child].wp[p];
     for (int a = 1; a < nch; a++) {
-      double v = T.nodes[E[a].child].wp[p];
+      double v = ND[E[a].child].wp[p];
       if (v > mx) mx = v;
     }
-    for (int a = 0; a < nch; a++) E[a].R += mx - T.nodes[E[a].child].wp[p];
+    for (int a = 0; a < nch; a++) E[a].R += mx - ND[E[a].child].wp[p];
   } else {
     CfrWide* W = cfr_wide(T, N.first_edge);
     for (int a = 0; a < nch; a++) {
-      const double* wp = T.nodes[E[a].child].wp;
+      const double* wp = ND[E[a].child].wp;
       double mx = wp[0];
       for (int p = 1; p < 6; p++) mx = (mx != mx || wp[p] != wp[p]) ? NAN : (wp[p] > mx ? wp[p] : mx);
       for (int p = 0; p < 6; p++) W[a].R[p] += mx - wp[p];
@@ -646,11 +739,16 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
   }
 }
 
-CIT_NOINLINE void cfr_backprop(CfrTree& T_in, int n, const double* reward, bool model) {
-  CfrTree& T = cfr_lds(T_in);
+// reward[6] is read before the walk (it may be a node's own pred array)
+CIT_NOINLINE void cfr_backprop(CfrTree& T_in, int n, double r0, double r1, double r2, double r3, double r4,
+                               double r5, int model) {
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(14);   // :276-290
+  n = cfr_u(n);
+  const double reward[6] = {r0, r1, r2, r3, r4, r5};
+  CfrNode* ND = cfr_nd(T);
   while (n >= 0) {
-    CfrNode& N = T.nodes[n];
+    CfrNode& N = ND[n];
     double s0 = 0.0;
     for (int k = 0; k < 6; k++) s0 += N.nv[k];
     if (T.training || s0 == 0.0 || !model)
@@ -662,26 +760,32 @@ CIT_NOINLINE void cfr_backprop(CfrTree& T_in, int n, const double* reward, bool 
     n = N.parent;
   }
 }
+CIT_HD void cfr_backprop_arr(CfrTree& T, int n, const double* rw, bool model) {
+  cfr_backprop(T, n, rw[0], rw[1], rw[2], rw[3], rw[4], rw[5], model ? 1 : 0);
+}
 
 // ---------------------------------------------------------------- drivers
-// cfr_train(iters) on the game in T.w0 (the root's game: skip_false_choice
-// mutates it, as the reference mutates the game passed to CFRNode).
-// Returns the root id.
-CIT_HD int cfr_train(CfrTree& T, int iters, bool root_skipped = false) {
-  int root = cfr_node(T, *T.w0, -1, 0, root_skipped);
+// cfr_train(iters) on the game in working row 0 (the root's game:
+// skip_false_choice mutates it, as the reference mutates the game passed to
+// CFRNode).  Returns the root id.
+CIT_HD int cfr_train(CfrTree& T_in, int iters, bool root_skipped = false) {
+  CfrTree& T = CFR_T(T_in);
+  CfrNode* ND = cfr_nd(T);
+  CfrEdge* ED = cfr_ed(T);
+  int root = cfr_u(cfr_node(T, 0, -1, 0, root_skipped ? 1 : 0));
   if (root < 0 || T.err) return root;
-  if (T.nodes[root].flags & NF_TERMINAL) return root;
+  if (ND[root].flags & NF_TERMINAL) return root;
   cfr_expand(T, root);
   int n = root;
   for (int it = 0; it < iters && !T.err; it++) {
     cfr_update_strategy(T, n);
-    int a = cfr_choose(T, n);
+    int a = cfr_u(cfr_choose(T, n));
     if (T.err) break;
-    n = T.edges[T.nodes[n].first_edge + a].child;
-    if (T.nodes[n].flags & NF_TERMINAL) {
+    n = ED[ND[n].first_edge + a].child;
+    if (ND[n].flags & NF_TERMINAL) {
       double rw[6] = {0, 0, 0, 0, 0, 0};
-      if (T.nodes[n].winner >= 0) rw[T.nodes[n].winner] = 1.0;
-      cfr_backprop(T, n, rw, false);
+      if (ND[n].winner >= 0) rw[ND[n].winner] = 1.0;
+      cfr_backprop_arr(T, n, rw, false);
       cfr_update_strategy(T, n);
       n = root;
     } else {
@@ -694,28 +798,30 @@ CIT_HD int cfr_train(CfrTree& T, int iters, bool root_skipped = false) {
 
 // action_choice(live=True) at the root (:67-91; game.py:312-317 for a role pick).
 CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
-  CfrTree& T = cfr_lds(T_in);
+  CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(15);
-  CfrNode& N = T.nodes[root];
+  root = cfr_u(root);
+  CfrNode& N = cfr_nd(T)[root];
   if (!(N.flags & NF_ROLE_PICK)) {
-    int a = cfr_choose(T, root);
+    int a = cfr_u(cfr_choose(T, root));
     if (T.err || a < 0) return mk(O_NUM_NAMES, 0);
-    return T.edges[N.first_edge + a].opt;
+    return cfr_ed(T)[N.first_edge + a].opt;
   }
-  CitGame& g = *T.w0;
-  copy_row(T, reinterpret_cast<uint32_t*>(&g), row_of(T, root));
-  eng_prepare(g, T.py, T.seer);
-  uint32_t le = 0;
-  int nl = eng_list(g, T.optbuf, CFR_OPT_CAP, le, T.seer);
-  T.err |= le;
+  CitGame& g = cfr_w(T, 0);
+  copy_row(T, w_row(T, 0), row_of(T, root));
+  eng_prepare(T, 0);
+  CfrCnt lc = cfr_ucnt(eng_list(T, 0));
+  int nl = lc.n;
+  T.err |= lc.err;
   int pid = g.gs_pid;
   const CfrWide* W = cfr_wide(T, N.first_edge);
+  const CitOpt* ob = cfr_glb(T.optbuf);
   double sum = 0.0;
-  for (int j = 0; j < nl; j++) sum += W[T.optbuf[j].a].S[pid];
-  int j = np_choice(T.np, [&](int i) { return W[T.optbuf[i].a].S[pid] / sum; }, nl, T.err);
-  copy_row(T, row_of(T, root), reinterpret_cast<const uint32_t*>(&g));
+  for (int j = 0; j < nl; j++) sum += W[ob[j].a].S[pid];
+  int j = np_choice(T.np, [&](int i) { return W[ob[i].a].S[pid] / sum; }, nl, T.err);
+  copy_row(T, row_of(T, root), w_row(T, 0));
   if (T.err || j < 0) return mk(O_NUM_NAMES, 0);
-  return T.optbuf[j];
+  return ob[j];
 }
 
 // ---------------------------------------------------------- cfr_pred (model)
@@ -727,14 +833,6 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
 // uses are requested: pred_node_value is read only at depth > max_depth, and a
 // node's prediction never changes (model_inference on the same game), so it is
 // computed once per node (expand_role_pick's last inference: player 5).
-enum { CP_INIT = 0, CP_RUN = 1, CP_WAIT = 2, CP_DONE = 3 };
-struct CfrState {                       // 64 B, persists in HBM between launches
-  int32_t n_nodes, n_edges, err, carry_outs;
-  int32_t cur, it, phase, pending;
-  int32_t root, orig, pad[6];
-};
-static_assert(sizeof(CfrState) == 64, "CfrState layout");
-
 CIT_HD void cfr_state_load(CfrTree& T, const CfrState& S) {
   T.n_nodes = S.n_nodes;
   T.n_edges = S.n_edges;
@@ -750,27 +848,34 @@ CIT_HD void cfr_state_save(const CfrTree& T, CfrState& S) {
 }
 
 CIT_NOINLINE void cfr_write_feat(CfrTree& T_in, int n, float* feat) {
-  CfrTree& T = cfr_lds(T_in);
+  CfrTree& T = CFR_T(T_in);
+  n = cfr_u(n);
   const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
-  int pid = (T.nodes[n].flags & NF_ROLE_PICK) ? 5 : -1;
+  int pid = (cfr_nd(T)[n].flags & NF_ROLE_PICK) ? 5 : -1;
   CFR_SYNC();
-  cit_encode_game(g, feat, pid);   // the whole team (identical stores): the engine's scans are wave-wide
+  cit_encode_game(g, cfr_glb(feat), pid);   // the whole team (identical stores): the engine's scans are wave-wide
   CFR_SYNC();
 }
 
-// One resumption.  w0 must hold the lane's game when S.phase == CP_INIT.
-// Returns 1 when suspended for an evaluation, 0 when done (S.phase == CP_DONE).
-CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_depth, const float* probs, float* feat,
-                              CitOpt& chosen, bool root_skipped = false) {
-  CfrTree& T = cfr_lds(T_in);
-  CfrState& S = cfr_lds(S_in);
+// One resumption.  Working row 0 must hold the lane's game when S.phase ==
+// CP_INIT.  Returns 1 when suspended for an evaluation, 0 when done (S.phase
+// == CP_DONE).
+CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_depth, const float* probs_in,
+                              float* feat, CitOpt& chosen, bool root_skipped = false) {
+  CfrTree& T = CFR_T(T_in);
+  CfrState& S = CFR_S(S_in);
+  iters = cfr_u(iters);
+  max_depth = cfr_u(max_depth);
+  const float* probs = cfr_glb(probs_in);
+  CfrNode* ND = cfr_nd(T);
+  CfrEdge* ED = cfr_ed(T);
   if (S.phase == CP_DONE) return 0;
   if (S.phase == CP_INIT) {
     S.orig = T.orig;
-    int root = cfr_node(T, *T.w0, -1, 0, root_skipped);
+    int root = cfr_u(cfr_node(T, 0, -1, 0, root_skipped ? 1 : 0));
     S.root = root;
     S.it = 0;
-    if (root < 0 || T.err || (T.nodes[root].flags & NF_TERMINAL)) {
+    if (root < 0 || T.err || (ND[root].flags & NF_TERMINAL)) {
       if (root >= 0 && !T.err) T.err |= CIT_ERR_VALUE;   // action_choice on a childless root raises
       S.phase = CP_DONE;
       chosen = mk(O_NUM_NAMES, 0);
@@ -781,10 +886,10 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
     S.phase = CP_RUN;
   } else if (S.phase == CP_WAIT) {
     int n = S.pending;
-    CfrNode& N = T.nodes[n];
+    CfrNode& N = ND[n];
     for (int k = 0; k < 6; k++) N.pred[k] = (double)(5.0f * probs[k]);   // model_reward_weights * wp (float32)
     N.flags |= NF_PRED;
-    cfr_backprop(T, n, N.pred, true);
+    cfr_backprop_arr(T, n, N.pred, true);
     cfr_update_strategy(T, n);
     S.cur = S.root;
     S.it++;
@@ -792,26 +897,26 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
   }
   while (S.it < iters && !T.err) {
     cfr_update_strategy(T, S.cur);
-    int a = cfr_choose(T, S.cur);
+    int a = cfr_u(cfr_choose(T, S.cur));
     if (T.err) break;
-    int n = T.edges[T.nodes[S.cur].first_edge + a].child;
-    CfrNode& N = T.nodes[n];
+    int n = ED[ND[S.cur].first_edge + a].child;
+    CfrNode& N = ND[n];
     if (N.depth > max_depth && !(N.flags & NF_TERMINAL)) {
       cfr_expand(T, n);
       if (T.err) break;
-      if (!(T.nodes[n].flags & NF_PRED)) {
+      if (!(ND[n].flags & NF_PRED)) {
         cfr_write_feat(T, n, feat);
         S.pending = n;
         S.phase = CP_WAIT;
         return 1;
       }
-      cfr_backprop(T, n, T.nodes[n].pred, true);
+      cfr_backprop_arr(T, n, ND[n].pred, true);
       cfr_update_strategy(T, n);
       S.cur = S.root;
     } else if (N.flags & NF_TERMINAL) {
       double rw[6] = {0, 0, 0, 0, 0, 0};
       if (N.winner >= 0) rw[N.winner] = 1.0;
-      cfr_backprop(T, n, rw, true);
+      cfr_backprop_arr(T, n, rw, true);
       cfr_update_strategy(T, n);
       S.cur = S.root;
     } else {
@@ -822,7 +927,7 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
   }
   if (!T.err) cfr_update_strategy(T, S.root);
   chosen = mk(O_NUM_NAMES, 0);
-  if (!T.err) chosen = cfr_live_choice(T, S.root);
+  if (!T.err) chosen = cfr_uopt(cfr_live_choice(T, S.root));
   S.phase = CP_DONE;
   return 0;
 }

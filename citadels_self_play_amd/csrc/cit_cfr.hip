@@ -1,11 +1,19 @@
 // MCCFR kernel + C ABI (include/citadels.h, "MCCFR" section): one tree per
 // 64-lane workgroup; see cit_cfr.h for the search itself.
+// Every MT19937 stream of this unit is an LDS stream run by the whole team.
+#define CIT_MT_COOP_ONLY 1
 #include <hip/hip_runtime.h>
 
 #include "../../include/citadels.h"
 #include "cit_cfr.h"
 
 #define ROW_W (CIT_GAME_BYTES / 4)
+
+#ifdef CFR_TREE_CLOCK
+// Per-tree start / end wall clock (100 MHz) of k_cfr_decide (measurement
+// builds only: tools/cfr_tree_clock.py).
+__device__ unsigned long long g_tree_clock[2 * 65536];
+#endif
 
 namespace {
 
@@ -20,6 +28,8 @@ __device__ __forceinline__ CitMT mt_stage_in(uint32_t* dst, const uint32_t* mt, 
   r.stride = 1;
   r.pos = idx[l];
   r.coop = 1;     // the team runs the search in lockstep: lane-parallel twist
+  r.win = 0;
+  r.win_base = -1;
   return r;
 }
 __device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, int B, long l) {
@@ -27,43 +37,49 @@ __device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, 
   for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) mt[(long)i * B + l] = src[i];
 }
 
+// The tree's LDS block (cit_cfr.h, cfr_ls): pool binding, streams, working rows.
+__device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx,
+                                           uint64_t* seer, int B, long l, uint8_t* pool, int node_cap, int edge_cap,
+                                           CitOpt* optbuf) {
+  CfrTree& T = cfr_ls.T;
+  cfr_tree_bind(T, pool, l, node_cap, edge_cap);
+  T.training = false;
+  T.py = mt_stage_in(cfr_ls.py, mt, idx, B, l);
+  T.np = mt_stage_in(cfr_ls.np, npmt, npidx, B, l);
+  T.seer = seer + l * CIT_SEER_MAX;
+  T.optbuf = optbuf + l * CFR_OPT_CAP;
+  T.w0 = reinterpret_cast<CitGame*>(cfr_ls.w[0]);
+  T.w1 = reinterpret_cast<CitGame*>(cfr_ls.w[1]);
+  T.tmp = cfr_ls.tmp;
+  T.lbuf = cfr_ls.lbuf;
+}
+
 // One MCCFR decision per workgroup: a 64-lane team runs the search on its
-// tree (node pool in HBM, working rows in LDS).
+// tree (node pool in HBM, working state in LDS).
 __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
                                                    uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
                                                    const int32_t* orig, uint8_t* pool,
                                                    int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen,
                                                    int32_t* stats) {
-  __shared__ __attribute__((aligned(16))) uint32_t w0s[ROW_W];
-  __shared__ __attribute__((aligned(16))) uint32_t w1s[ROW_W];
-  __shared__ __attribute__((aligned(16))) uint8_t tmps[128];
-  __shared__ __attribute__((aligned(16))) CitOpt lbufs[CFR_LBUF];
   long l = blockIdx.x;
   if (l >= B) return;
+#ifdef CFR_TREE_CLOCK
+  unsigned long long tc0 = wall_clock64();
+#endif
   cfr_prof_reset();
-  __shared__ CfrTree T;     // shared: the wavefront's lanes update it in lockstep
-  cfr_tree_bind(T, pool, l, node_cap, edge_cap);
+  CfrTree& T = cfr_ls.T;
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf);
   T.n_nodes = T.n_edges = 0;
-  T.training = false;
-  __shared__ uint32_t pys[CIT_MT_N], nps[CIT_MT_N];
-  T.py = mt_stage_in(pys, mt, idx, B, l);
-  T.np = mt_stage_in(nps, npmt, npidx, B, l);
-  T.seer = seer + l * CIT_SEER_MAX;
-  T.optbuf = optbuf + l * CFR_OPT_CAP;
-  T.w0 = reinterpret_cast<CitGame*>(w0s);
-  T.w1 = reinterpret_cast<CitGame*>(w1s);
-  T.tmp = tmps;
-  T.lbuf = lbufs;
   T.err = 0;
   T.carry_outs = 0;
-  copy_row(T, w0s, games + l * ROW_W);
-  T.orig = orig ? orig[l] : T.w0->gs_pid;
+  copy_row(T, cfr_ls.w[0], games + l * ROW_W);
+  T.orig = orig ? orig[l] : cfr_w(T, 0).gs_pid;
   int root = cfr_train(T, iters, (flags & CIT_CFR_ROOT_SKIPPED) != 0);
   CitOpt c = mk(O_NUM_NAMES, 0);
-  if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
+  if (root >= 0 && !T.err) c = cfr_uopt(cfr_live_choice(T, root));
   if (root >= 0) copy_row(T, games + l * ROW_W, row_of(T, root));
-  mt_stage_out(pys, mt, B, l);
-  mt_stage_out(nps, npmt, B, l);
+  mt_stage_out(cfr_ls.py, mt, B, l);
+  mt_stage_out(cfr_ls.np, npmt, B, l);
   if (threadIdx.x == 0) {
     chosen[l] = c;
     idx[l] = T.py.pos;
@@ -73,6 +89,12 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
     stats[5 * l + 2] = T.n_edges;
     stats[5 * l + 3] = (int)T.carry_outs;
     stats[5 * l + 4] = (int)T.err;
+#ifdef CFR_TREE_CLOCK
+    if (l < 65536) {
+      g_tree_clock[2 * l] = tc0;
+      g_tree_clock[2 * l + 1] = wall_clock64();
+    }
+#endif
   }
   cfr_prof_flush();
 }
@@ -84,43 +106,30 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
                                                       const int32_t* orig, int max_depth, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
                                                       CfrState* state, const float* probs, float* feat,
                                                       CitOpt* chosen, int32_t* waiting) {
-  __shared__ __attribute__((aligned(16))) uint32_t w0s[ROW_W];
-  __shared__ __attribute__((aligned(16))) uint32_t w1s[ROW_W];
-  __shared__ __attribute__((aligned(16))) uint8_t tmps[128];
-  __shared__ __attribute__((aligned(16))) CitOpt lbufs[CFR_LBUF];
   long l = blockIdx.x;
   if (l >= B) return;
-  __shared__ CfrState S;
+  CfrState& S = cfr_ls.S;
   S = state[l];             // every lane stores the same value
   if (S.phase == CP_DONE) return;
-  __shared__ CfrTree T;     // shared: the wavefront's lanes update it in lockstep
-  cfr_tree_bind(T, pool, l, node_cap, edge_cap);
-  T.training = false;
-  __shared__ uint32_t pys[CIT_MT_N], nps[CIT_MT_N];
-  T.py = mt_stage_in(pys, mt, idx, B, l);
-  T.np = mt_stage_in(nps, npmt, npidx, B, l);
-  T.seer = seer + l * CIT_SEER_MAX;
-  T.optbuf = optbuf + l * CFR_OPT_CAP;
-  T.w0 = reinterpret_cast<CitGame*>(w0s);
-  T.w1 = reinterpret_cast<CitGame*>(w1s);
-  T.tmp = tmps;
-  T.lbuf = lbufs;
+  CfrTree& T = cfr_ls.T;
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf);
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;
     T.carry_outs = 0;
-    copy_row(T, w0s, games + l * ROW_W);
-    T.orig = orig ? orig[l] : T.w0->gs_pid;
+    copy_row(T, cfr_ls.w[0], games + l * ROW_W);
+    T.orig = orig ? orig[l] : cfr_w(T, 0).gs_pid;
   } else {
     cfr_state_load(T, S);
   }
   CitOpt c;
   int r = cfr_pred_run(T, S, iters, max_depth, probs + 6 * l, feat + (long)CIT_FEAT * l, c,
                        (flags & CIT_CFR_ROOT_SKIPPED) != 0);
+  r = cfr_u(r);
   cfr_state_save(T, S);
   if (!r && S.root >= 0) copy_row(T, games + l * ROW_W, row_of(T, S.root));
-  mt_stage_out(pys, mt, B, l);
-  mt_stage_out(nps, npmt, B, l);
+  mt_stage_out(cfr_ls.py, mt, B, l);
+  mt_stage_out(cfr_ls.np, npmt, B, l);
   if (threadIdx.x == 0) {
     state[l] = S;
     if (!r) chosen[l] = c;
@@ -171,6 +180,12 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
                      (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting);
   CHECK_LAUNCH();
 }
+
+#ifdef CFR_TREE_CLOCK
+int cit_tree_clock_read(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tree_clock), sizeof(unsigned long long) * 2 * n);
+}
+#endif
 
 #if defined(CIT_PROF)
 int cit_prof_read(unsigned long long* out) {

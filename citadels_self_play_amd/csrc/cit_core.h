@@ -352,7 +352,10 @@ CIT_HD uint32_t mt_temper(uint32_t y) {
 CIT_HD uint32_t mt_next(CitMT& r) {
   uint32_t i = r.pos;
   if (i >= CIT_MT_N) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(CIT_MT_COOP_ONLY)
+    mt_twist_coop((cit_lds_u32*)r.mt);   // a unit whose every stream is an LDS coop stream
+    r.win_base = -1;
+#elif defined(__HIP_DEVICE_COMPILE__)
     if (r.coop) {
       mt_twist_coop((cit_lds_u32*)r.mt);
       r.win_base = -1;
@@ -365,7 +368,9 @@ CIT_HD uint32_t mt_next(CitMT& r) {
     i = 0;
   }
   r.pos = i + 1;
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(CIT_MT_COOP_ONLY)
+  return mt_temper(((const cit_lds_u32*)r.mt)[i]);
+#elif defined(__HIP_DEVICE_COMPILE__)
   if (r.coop == CIT_MT_WINDOW) {
     int b = (int)(i & ~63u);
     if (b != r.win_base) {

@@ -84,19 +84,22 @@ struct CfrTree {
   uint32_t carry_outs;
 };
 
-// Node pool of one tree: [node_cap CfrNode][edge_cap CfrEdge][node_cap rows];
-// B trees are B consecutive pools.  Sizes are 64-bit: a cfr_train(200000)
-// tree needs ~0.5-1 GB.
+// Node pool of one tree: [node_cap CfrNode][edge_cap CfrEdge][pad to 16 B]
+// [node_cap rows]; B trees are B consecutive pools (every pool and row starts
+// 16-byte aligned, so rows move as 16-byte words).  Sizes are 64-bit: a
+// cfr_train(200000) tree needs ~0.5-1 GB.
+CIT_HD int64_t cfr_rows_offset(int node_cap, int edge_cap) {
+  int64_t o = (int64_t)node_cap * (int64_t)sizeof(CfrNode) + (int64_t)edge_cap * (int64_t)sizeof(CfrEdge);
+  return (o + 15) & ~(int64_t)15;
+}
 CIT_HD int64_t cfr_pool_bytes(int node_cap, int edge_cap) {
-  return (int64_t)node_cap * (int64_t)sizeof(CfrNode) + (int64_t)edge_cap * (int64_t)sizeof(CfrEdge) +
-         (int64_t)node_cap * CIT_GAME_BYTES;
+  return cfr_rows_offset(node_cap, edge_cap) + (int64_t)node_cap * CIT_GAME_BYTES;
 }
 CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, long l, int node_cap, int edge_cap) {
   uint8_t* base = pool + cfr_pool_bytes(node_cap, edge_cap) * (int64_t)l;
   T.nodes = reinterpret_cast<CfrNode*>(base);
   T.edges = reinterpret_cast<CfrEdge*>(base + (int64_t)node_cap * (int64_t)sizeof(CfrNode));
-  T.rows = reinterpret_cast<uint32_t*>(base + (int64_t)node_cap * (int64_t)sizeof(CfrNode) +
-                                       (int64_t)edge_cap * (int64_t)sizeof(CfrEdge));
+  T.rows = reinterpret_cast<uint32_t*>(base + cfr_rows_offset(node_cap, edge_cap));
   T.node_cap = node_cap;
   T.edge_cap = edge_cap;
 }
@@ -167,12 +170,14 @@ CIT_HD CitOpt cfr_uopt(const CitOpt& o) { return o; }
 // bound in CfrTree.
 #if defined(__HIPCC__)
 struct CfrLds {
+  uint32_t w[2][CIT_GAME_BYTES / 4];
+  CitOpt lbuf[CFR_LBUF];
+  double sbuf[CFR_OPT_CAP], cbuf[CFR_OPT_CAP];   // update_strategy: S, CS of node `cnode`
+  uint32_t py[CIT_MT_N], np[CIT_MT_N];
   CfrTree T;
   CfrState S;
-  uint32_t w[2][CIT_GAME_BYTES / 4];
-  uint32_t py[CIT_MT_N], np[CIT_MT_N];
-  CitOpt lbuf[CFR_LBUF];
-  uint8_t tmp[128];
+  int cnode, cnch;                                // node (and its child count) whose normalised CS is in cbuf (-1: none)
+  uint8_t tmp[CIT_SAMPLE_SCRATCH];
 };
 static __shared__ __attribute__((aligned(16))) CfrLds cfr_ls;
 #endif
@@ -234,7 +239,18 @@ struct CitProf {
     }
   }
 };
-#define CIT_PROF_SCOPE(i) CitProf _cit_prof_scope(i)
+// CIT_PROF_MASK selects the scopes that are timed (bit i = scope i), so a
+// profile can time a few scopes at a time with little perturbation.
+#ifndef CIT_PROF_MASK
+#define CIT_PROF_MASK 0xffff
+#endif
+struct CitProfOff {
+  __device__ explicit CitProfOff(int) {}
+};
+#define CIT_PROF_SCOPE(i)                                                         \
+  typename cit_prof_sel<((CIT_PROF_MASK >> (i)) & 1) != 0>::type _cit_prof_scope(i)
+template <bool On> struct cit_prof_sel { typedef CitProf type; };
+template <> struct cit_prof_sel<false> { typedef CitProfOff type; };
 __device__ inline void cfr_prof_reset() {
   if (threadIdx.x < 32) cit_prof_lds[threadIdx.x] = 0;
   __syncthreads();
@@ -304,7 +320,18 @@ CIT_HD void copy_row(const CfrTree& T, uint32_t* dst, const uint32_t* src) {
   (void)T;
   CIT_PROF_SCOPE(6);
   CFR_SYNC();
+#if CIT_WAVE
+  {   // 97 16-byte words: lanes 0..63, then 0..32; both loads issued before the stores
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    const int l = CFR_LANE, hi = l + 64 < CIT_GAME_BYTES / 16;
+    uint4 a = s4[l], b = hi ? s4[l + 64] : a;
+    d4[l] = a;
+    if (hi) d4[l + 64] = b;
+  }
+#else
   for (int i = CFR_LANE; i < CIT_GAME_BYTES / 4; i += CFR_TEAM) dst[i] = src[i];
+#endif
   CFR_SYNC();
 }
 
@@ -484,6 +511,22 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
   int id = T.n_nodes++;
   CfrNode& N = cfr_nd(T)[id];
+#if CIT_WAVE
+  {   // the header's 6 words and the 36 zero words of nv / wp / pred, one store per lane
+    uint32_t hw[6];
+    hw[0] = (uint32_t)parent;
+    hw[1] = (uint32_t)-1;
+    hw[2] = 0;                                   // n_children, edge_cap
+    hw[3] = (uint32_t)(uint16_t)depth | ((uint32_t)(uint8_t)w.gs_pid << 16) | ((uint32_t)w.gs_state << 24);
+    hw[4] = (uint32_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0)) |
+            ((uint32_t)(uint8_t)w.winner << 8);
+    hw[5] = 0;
+    const int l = CFR_LANE;
+    uint32_t v = 0;
+    for (int k = 0; k < 6; k++) v = l == k ? hw[k] : v;
+    if (l < (int)(sizeof(CfrNode) / 4)) reinterpret_cast<uint32_t*>(&N)[l] = v;
+  }
+#else
   N.parent = parent;
   N.first_edge = -1;
   N.n_children = 0;
@@ -494,6 +537,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   N.flags = (uint8_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0));
   N.winner = w.winner;
   for (int k = 0; k < 6; k++) N.nv[k] = N.wp[k] = N.pred[k] = 0.0;
+#endif
   copy_row(T, row_of(T, id), w_row(T, which));
   return id;
 }
@@ -648,6 +692,36 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
   int nch = N.n_children;
   if (nch == 0) return;
   CfrEdge* E = cfr_ed(T) + N.first_edge;
+#if CIT_WAVE
+  if (!(N.flags & NF_ROLE_PICK)) {
+    // lane a (a + 64, ...) owns edge a; the numpy sums run in their serial
+    // order over LDS copies (cbuf keeps the normalised CS for cfr_choose)
+    double* sb = cfr_ls.sbuf;
+    double* cb = cfr_ls.cbuf;
+    if (nch > CFR_OPT_CAP) { T.err |= CIT_ERR_OVERFLOW; return; }
+    const int l = CFR_LANE;
+    for (int a = l; a < nch; a += 64) sb[a] = exp((-E[a].R) * CFR_LN13);
+    CFR_SYNC();
+    double tot = np_sum([sb](int i) { return sb[i]; }, nch, T.err);
+    for (int a = l; a < nch; a += 64) {
+      double v = tot > 0 ? sb[a] / tot : 1.0 / nch;
+      E[a].S = v;
+      cb[a] = E[a].CS + v;
+    }
+    CFR_SYNC();
+    double cs = np_sum([cb](int i) { return cb[i]; }, nch, T.err);
+    CFR_SYNC();
+    for (int a = l; a < nch; a += 64) {
+      double v = cb[a] / cs;
+      E[a].CS = v;
+      cb[a] = v;
+    }
+    CFR_SYNC();
+    cfr_ls.cnode = n;
+    cfr_ls.cnch = nch;
+    return;
+  }
+#endif
   if (!(N.flags & NF_ROLE_PICK)) {
     for (int a = 0; a < nch; a++) E[a].S = exp((-E[a].R) * CFR_LN13);
     double tot = np_sum([E](int i) { return E[i].S; }, nch, T.err);
@@ -691,6 +765,13 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
   int nch = N.n_children;
   const CfrEdge* E = cfr_ed(T) + (N.first_edge < 0 ? 0 : N.first_edge);
   if (!(N.flags & NF_ROLE_PICK)) {
+#if CIT_WAVE
+    if (cfr_ls.cnode == n && cfr_ls.cnch == nch) {   // update_strategy(n) left CS in LDS
+      const double* cb = cfr_ls.cbuf;
+      double tot = np_sum([cb](int i) { return cb[i]; }, nch, T.err);
+      return np_choice(T.np, [cb, tot](int i) { return cb[i] / tot; }, nch, T.err);
+    }
+#endif
     double tot = np_sum([E](int i) { return E[i].CS; }, nch, T.err);
     return np_choice(T.np, [E, tot](int i) { return E[i].CS / tot; }, nch, T.err);
   }

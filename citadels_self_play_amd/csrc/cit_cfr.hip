@@ -42,6 +42,7 @@ __device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t
                                            uint64_t* seer, int B, long l, uint8_t* pool, int node_cap, int edge_cap,
                                            CitOpt* optbuf) {
   CfrTree& T = cfr_ls.T;
+  cfr_ls.cnode = -1;
   cfr_tree_bind(T, pool, l, node_cap, edge_cap);
   T.training = false;
   T.py = mt_stage_in(cfr_ls.py, mt, idx, B, l);

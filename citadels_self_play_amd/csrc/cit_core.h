@@ -38,6 +38,8 @@
 __device__ __forceinline__ int cit_lane() { return (int)__lane_id(); }
 __device__ __forceinline__ uint64_t cit_ballot(bool p) { return (uint64_t)__ballot(p); }
 __device__ __forceinline__ int cit_readlane(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
+__device__ __forceinline__ int cit_writelane(int v, int val, int i) { return (int)__lane_id() == i ? val : v; }
+__device__ __forceinline__ uint64_t cit_below() { return (1ull << __lane_id()) - 1; }   // lanes under this one
 extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_or_u32(unsigned int);
 __device__ __forceinline__ uint64_t cit_wave_or64(uint64_t v) {
   return ((uint64_t)__ockl_wfred_or_u32((unsigned int)(v >> 32)) << 32) | __ockl_wfred_or_u32((unsigned int)v);
@@ -368,9 +370,7 @@ CIT_HD uint32_t mt_next(CitMT& r) {
     i = 0;
   }
   r.pos = i + 1;
-#if defined(__HIP_DEVICE_COMPILE__) && defined(CIT_MT_COOP_ONLY)
-  return mt_temper(((const cit_lds_u32*)r.mt)[i]);
-#elif defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
   if (r.coop == CIT_MT_WINDOW) {
     int b = (int)(i & ~63u);
     if (b != r.win_base) {
@@ -380,7 +380,11 @@ CIT_HD uint32_t mt_next(CitMT& r) {
     }
     return (uint32_t)__builtin_amdgcn_readlane((int)r.win, (int)(i & 63u));
   }
+#if defined(CIT_MT_COOP_ONLY)
+  return mt_temper(((const cit_lds_u32*)r.mt)[i]);
+#else
   if (r.coop) return mt_temper(((const cit_lds_u32*)r.mt)[i]);   // coop streams live in LDS (stride 1)
+#endif
 #endif
   return mt_temper(mt_word(r, (int)i));
 }
@@ -401,3 +405,27 @@ CIT_HD double mt_random(CitMT& r) {
   uint32_t a = mt_next(r) >> 5, b = mt_next(r) >> 6;
   return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
 }
+
+#if CIT_WAVE
+// A burst of draws from an LDS stream through a register window (CitMT
+// CIT_MT_WINDOW): a copy of the stream whose draws are readlanes of 64
+// tempered words; cit_mt_unwindow() hands the position (and, for a stream
+// that already was a window, the window) back.  Only for coop streams
+// (r.coop != 0: the words are in LDS and the whole wave runs the owner).
+CIT_HD CitMT cit_mt_window(const CitMT& r) {
+  CitMT w = r;
+  if (w.coop != CIT_MT_WINDOW) {
+    w.coop = CIT_MT_WINDOW;
+    w.win = 0;
+    w.win_base = -1;
+  }
+  return w;
+}
+CIT_HD void cit_mt_unwindow(CitMT& r, const CitMT& w) {
+  r.pos = w.pos;
+  if (r.coop == CIT_MT_WINDOW) {
+    r.win = w.win;
+    r.win_base = w.win_base;
+  }
+}
+#endif

@@ -180,9 +180,34 @@ CIT_HD int deck_take_like(CitGame& g, int c) {
   }
   return c;
 }
-// random.shuffle (Lib/random.py:380-392) over any indexable sequence
+// random.shuffle (Lib/random.py:380-392) over any indexable sequence.
+// Wave path (a coop LDS stream, n <= 128, a sequence in shared memory; a
+// lane-private array keeps the serial loop): the sequence moves into two VGPRs
+// (lane i holds elements i and 64 + i), the draws come through a register
+// window and each swap is two readlanes and two writelanes, so the serial
+// chain has no memory round trip; the lanes store the result back.
 template <class At>
 CIT_HD void shuffle_seq(CitMT& rng, int n, At at) {
+#if CIT_WAVE
+  if (n <= 128 && rng.coop && !__builtin_amdgcn_is_private((const void*)&at(0))) {
+    const int l = cit_lane();
+    int v0 = l < n ? at(l) : 0, v1 = l + 64 < n ? at(l + 64) : 0;
+    CitMT w = cit_mt_window(rng);
+    for (int i = n - 1; i > 0; i--) {
+      int j = (int)mt_randbelow(w, (uint32_t)(i + 1));
+      int ai = i < 64 ? cit_readlane(v0, i) : cit_readlane(v1, i - 64);
+      int aj = j < 64 ? cit_readlane(v0, j) : cit_readlane(v1, j - 64);
+      if (i < 64) v0 = cit_writelane(v0, aj, i);
+      else v1 = cit_writelane(v1, aj, i - 64);
+      if (j < 64) v0 = cit_writelane(v0, ai, j);
+      else v1 = cit_writelane(v1, ai, j - 64);
+    }
+    cit_mt_unwindow(rng, w);
+    if (l < n) at(l) = (uint8_t)v0;
+    if (l + 64 < n) at(l + 64) = (uint8_t)v1;
+    return;
+  }
+#endif
   for (int i = n - 1; i > 0; i--) {
     int j = (int)mt_randbelow(rng, (uint32_t)(i + 1));
     uint8_t t = at(i);
@@ -1881,10 +1906,207 @@ CIT_HD void kr_strip(const CitGame& g, uint16_t* kr, int role) {
   }
 }
 
+#define CIT_SAMPLE_SCRATCH 256   // bytes of `unk` scratch cit_sample_private needs
+
+#if CIT_WAVE
+// Append src(i), i < cnt (<= 128), to dst[base..) skipping CIT_NO_CARD (the
+// reference's add_card drops the "Deck Empty" sentinel); returns the count
+// appended.  Lanes i and 64 + i move one element each.
+template <class Src, class Dst>
+CIT_HD int wave_append(Dst dst, int base, int cnt, Src src) {
+  const int l = cit_lane();
+  const uint64_t below = cit_below();
+  int c0 = l < cnt ? src(l) : CIT_NO_CARD, c1 = l + 64 < cnt ? src(l + 64) : CIT_NO_CARD;
+  uint64_t m0 = cit_ballot(c0 != CIT_NO_CARD), m1 = cit_ballot(c1 != CIT_NO_CARD);
+  int n0 = __popcll(m0);
+  if (c0 != CIT_NO_CARD) dst(base + __popcll(m0 & below)) = (uint8_t)c0;
+  if (c1 != CIT_NO_CARD) dst(base + n0 + __popcll(m1 & below)) = (uint8_t)c1;
+  return n0 + __popcll(m1);
+}
+
+// cit_sample_private for a wave running the game uniformly with a coop (LDS)
+// stream: the same draws in the same order (through a register window), the
+// list work spread over the lanes.  `unk` holds >= CIT_SAMPLE_SCRATCH bytes:
+// the unknown cards [0, 80) and the per-type removal counts u32[40] at 80.
+CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitMT& rng, uint8_t* unk) {
+  const int l = cit_lane();
+  const uint64_t below = cit_below();
+  CitPlayer& PC = g.pl[orig];
+  CitMT w = cit_mt_window(rng);
+  // lane e: HandKnowledge entry e, its pool offset (exclusive scan of len)
+  const int nkh = g.n_kh;
+  const int le = l < nkh ? l : 0;
+  const int kowner = g.kh[le].owner, ktarget = g.kh[le].target, kflags = g.kh[le].conf_flags;
+  const int klen = l < nkh ? g.kh[le].len : 0;
+  int koff = 0;
+  for (int j = 0; j < nkh; j++) koff += j < l ? cit_readlane(klen, j) : 0;
+  const bool mine = l < nkh && kowner == orig;
+  // hk.used with probability (confidence-1)*0.2, entries in order (:217-222)
+  uint64_t used = 0;
+  for (uint64_t m = cit_ballot(mine); m; m &= m - 1) {
+    int e = __ffsll((unsigned long long)m) - 1;
+    double r = mt_random(w);
+    int conf = cit_readlane(kflags, e) & 15;
+    if ((double)(conf - 1) * 0.2 > r) used |= 1ull << e;
+  }
+  const bool uu = mine && ((used >> l) & 1);
+  if (mine) g.kh[l].conf_flags = (uint8_t)((kflags & ~0x20) | (uu ? 0x20 : 0));
+  // get_unknown_cards (:183-213): removals per type, then drop the first k_t
+  // used cards of each type t
+  uint32_t* kt = reinterpret_cast<uint32_t*>(unk + CIT_USED_CAP);
+  if (l < 40) kt[l] = 0;
+  __syncthreads();
+  for (int pass = 0; pass < 2; pass++) {
+    int p = pass * 4 + (l >> 4), i = l & 15;
+    if (p < CIT_NP) {
+      if (i < g.pl[p].n_build) atomicAdd(&kt[card_type(g.pl[p].build[i])], 1u);
+      if (i < g.pl[p].n_museum) atomicAdd(&kt[card_type(g.pl[p].museum[i])], 1u);
+    }
+  }
+  if (l < PC.n_hand) atomicAdd(&kt[card_type(PC.hand[l])], 1u);
+  for (uint64_t m = cit_ballot(uu); m; m &= m - 1) {
+    int e = __ffsll((unsigned long long)m) - 1;
+    int off = cit_readlane(koff, e), len = cit_readlane(klen, e);
+    for (int i = l; i < len; i += 64) atomicAdd(&kt[card_type(g.kh_pool[off + i])], 1u);
+  }
+  __syncthreads();
+  const int nuc = g.n_used_cards;
+  const bool v0 = l < nuc, v1 = l + 64 < nuc;
+  const int c0 = v0 ? g.used_cards[l] : 0, c1 = v1 ? g.used_cards[l + 64] : 0;
+  const int t0 = card_type(c0), t1 = card_type(c1);
+  int rk0 = 0, rk1 = 0;                          // rank among the earlier used cards of the same type
+  uint64_t rem0 = cit_ballot(v0), rem1 = cit_ballot(v1);
+  while (rem0 | rem1) {
+    int t = rem0 ? cit_readlane(t0, __ffsll((unsigned long long)rem0) - 1)
+                 : cit_readlane(t1, __ffsll((unsigned long long)rem1) - 1);
+    uint64_t m0 = cit_ballot(v0 && t0 == t), m1 = cit_ballot(v1 && t1 == t);
+    if (t0 == t) rk0 = __popcll(m0 & below);
+    if (t1 == t) rk1 = __popcll(m0) + __popcll(m1 & below);
+    rem0 &= ~m0;
+    rem1 &= ~m1;
+  }
+  const bool k0 = v0 && rk0 >= (int)kt[t0], k1 = v1 && rk1 >= (int)kt[t1];
+  const uint64_t km0 = cit_ballot(k0), km1 = cit_ballot(k1);
+  const int nk0 = __popcll(km0);
+  __syncthreads();
+  if (k0) unk[__popcll(km0 & below)] = (uint8_t)c0;
+  if (k1) unk[nk0 + __popcll(km1 & below)] = (uint8_t)c1;
+  const int nu = nk0 + __popcll(km1);
+  __syncthreads();
+  int head = 0;                                  // unk[head..nu): the undealt unknown cards
+  auto deck_slot = [&g](int i) -> uint8_t& { return g.deck[i & (CIT_DECK_CAP - 1)]; };
+  // sample_deck (:245-262): lighthouse knowledge first, then shuffled unknowns
+  {
+    int n = g.n_deck, nd = 0;
+    uint64_t lm = cit_ballot(uu && ktarget == -1);
+    g.n_deck = 0;
+    g.deck_head = 0;
+    if (lm) {
+      int e = __ffsll((unsigned long long)lm) - 1;
+      int lo = cit_readlane(koff, e), ll = cit_readlane(klen, e);
+      int kk = ll < n ? ll : n;
+      nd = wave_append(deck_slot, 0, kk, [&g, lo](int i) { return (int)g.kh_pool[lo + i]; });
+      n -= kk;
+    }
+    shuffle_arr(w, unk, nu);
+    __syncthreads();
+    int m = n < nu ? n : nu;
+    nd += wave_append(deck_slot, nd, m, [unk](int i) { return (int)unk[i]; });
+    head = m;
+    g.n_deck = (uint8_t)nd;
+  }
+  // sample_warrants_and_blackmails (:321-336): the marked roles (<= 8) as
+  // nibbles of one word, shuffled; the first is the real one
+  for (int which = 0; which < 2; which++) {
+    int shift = which == 0 ? RP_BLACKMAIL_SHIFT : RP_WARRANT_SHIFT;
+    uint32_t pk = 0;
+    int nk = 0;
+    for (int r = 0; r < 8; r++)
+      if ((g.rp[r] >> shift) & 3) pk |= (uint32_t)r << (4 * nk++);
+    if (!nk) continue;
+    for (int i = nk - 1; i > 0; i--) {
+      int j = (int)mt_randbelow(w, (uint32_t)(i + 1));
+      uint32_t ai = (pk >> (4 * i)) & 15, aj = (pk >> (4 * j)) & 15;
+      pk &= ~((15u << (4 * i)) | (15u << (4 * j)));
+      pk |= (aj << (4 * i)) | (ai << (4 * j));
+    }
+    int real = (int)(pk & 15);
+    for (int i = 0; i < nk; i++) {
+      int r = (int)((pk >> (4 * i)) & 15);
+      g.rp[r] = (uint8_t)((g.rp[r] & ~(3u << shift)) | ((r == real ? WB_REAL : WB_FAKE) << shift));
+    }
+  }
+  uint16_t kr[CIT_NP];
+  for (int j = 0; j < CIT_NP; j++) kr[j] = PC.kr[j];
+  if (role_sample) {   // remove_role_and_smaller_id_roles_from_role_knowledge_if_unconfirmed (:304-310)
+    int role = g.pl[g.gs_pid].role;
+    kr_strip(g, kr, role);
+    if (role != ROLE_NONE) {
+      int rr = role_rank(g, role);
+      for (int rid = 0; rid < 8; rid++)
+        if (rid < rr) kr_strip(g, kr, g.roles[rid]);
+    }
+  }
+  for (int p = 0; p < CIT_NP; p++) {
+    CitPlayer& Q = g.pl[p];
+    if (p != orig) {   // sample_cards_for_opponent (:264-280)
+      int n = Q.n_hand, nh = 0;
+      uint64_t hm = cit_ballot(uu && ktarget == p);
+      if (hm) {
+        int e = __ffsll((unsigned long long)hm) - 1;
+        int ho = cit_readlane(koff, e), hl = cit_readlane(klen, e);
+        int kk = hl < n ? hl : n;
+        nh = wave_append([&Q](int i) -> uint8_t& { return Q.hand[i & (CIT_HAND_CAP - 1)]; }, 0, kk,
+                         [&g, ho](int i) { return (int)g.kh_pool[ho + i]; });
+        n -= kk;
+      }
+      int m = n < nu - head ? n : nu - head;
+      nh += wave_append([&Q](int i) -> uint8_t& { return Q.hand[i & (CIT_HAND_CAP - 1)]; }, nh, m,
+                        [unk, head](int i) { return (int)unk[head + i]; });
+      head += m;
+      Q.n_hand = (uint8_t)nh;
+    }
+    // sample_roles_for_opponent (:283-295)
+    if (role_sample && p != orig && p != g.gs_pid && g.gs_state != 0) {
+      int cnt = 0;
+      for (int rid = -1; rid < 8; rid++) cnt += (kr[p] >> (rid + 1)) & 1;
+      int k = (int)mt_randbelow(w, (uint32_t)cnt);
+      if (cnt) {
+        int rid = -1;
+        for (int q = -1; q < 8; q++)
+          if ((kr[p] >> (q + 1)) & 1) {
+            if (k == 0) { rid = q; break; }
+            k--;
+          }
+        Q.role = (uint8_t)role_of_id(g, rid);
+        kr_strip(g, kr, Q.role);
+      } else {   // the IndexError band-aid: first role id not in used_roles
+        int pick = -1;
+        for (int rid = 0; rid < 8 && pick < 0; rid++) {
+          bool in = false;
+          for (int u = 0; u < g.n_used_roles && u < CIT_NP; u++) in |= g.used_roles[u] == rid;
+          if (!in) pick = rid;
+        }
+        if (pick < 0) { g.err |= CIT_ERR_INDEX; cit_mt_unwindow(rng, w); return; }   // StopIteration
+        Q.role = g.roles[pick];
+      }
+    }
+  }
+  if (role_sample && g.gs_state != 0) refresh_used_roles(g);
+  cit_mt_unwindow(rng, w);
+}
+#endif
+
 // Game.sample_private_information(players[orig], role_sample) (game.py:215-339):
-// resample everything `orig` cannot see.  `unk` is >= CIT_USED_CAP + 40 bytes
-// of scratch (LDS on the device).
+// resample everything `orig` cannot see.  `unk` is >= CIT_SAMPLE_SCRATCH
+// bytes of scratch (LDS on the device).
 CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rng, uint8_t* unk) {
+#if CIT_WAVE
+  if (rng.coop) {
+    cit_sample_private_wave(g, orig, role_sample, rng, unk);
+    return;
+  }
+#endif
   CitPlayer& PC = g.pl[orig];
   // hk.used with probability (confidence-1)*0.2 (:217-222)
   for (int e = 0; e < g.n_kh; e++) {

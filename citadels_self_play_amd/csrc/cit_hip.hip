@@ -139,8 +139,8 @@ __global__ __launch_bounds__(64) void k_count_options(uint32_t* games, uint32_t*
 // Game.sample_private_information(players[orig[l]], role_sample) per lane.
 __global__ __launch_bounds__(64) void k_determinize(uint32_t* games, uint32_t* mt, uint32_t* idx, int B,
                                                    const int32_t* orig, int role_sample) {
-  __shared__ __attribute__((aligned(16))) uint8_t unk[CIT_USED_CAP + 48];
-  uniform_game<false, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
+  __shared__ __attribute__((aligned(16))) uint8_t unk[CIT_SAMPLE_SCRATCH];
+  uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {   // MT in LDS: the wave path
     int o = orig[l];
     if (o < 0 || o >= CIT_NP) {
       g.err |= CIT_ERR_INDEX;

@@ -160,7 +160,7 @@ void cith_count_options(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer,
 }
 
 void cith_determinize(CitGame* g, uint32_t* mt, uint32_t* idx, int B, const int* orig, int role_sample) {
-  uint8_t unk[CIT_USED_CAP + 48];
+  uint8_t unk[CIT_SAMPLE_SCRATCH];
   for (int l = 0; l < B; l++) {
     CitMT r = lane_rng(mt, idx, B, l);
     cit_sample_private(g[l], orig[l], role_sample != 0, r, unk);
@@ -190,7 +190,7 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
                      int iters, int flags, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen, int* stats) {
   CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
-  uint8_t tmp[128];
+  uint8_t tmp[CIT_SAMPLE_SCRATCH];
   CitOpt lbuf[CFR_LBUF];
   for (int l = 0; l < B; l++) {
     CfrTree T;
@@ -240,7 +240,7 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
                        CfrState* st, const float* probs, float* feat, CitOpt* chosen) {
   CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
   CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
-  uint8_t tmp[128];
+  uint8_t tmp[CIT_SAMPLE_SCRATCH];
   CitOpt lbuf[CFR_LBUF];
   int waiting = 0;
   for (int l = 0; l < B; l++) {

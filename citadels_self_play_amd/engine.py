@@ -391,7 +391,8 @@ class GameBatch:
         nb, eb = self.node_cap * NODE_DT.itemsize, self.edge_cap * EDGE_DT.itemsize
         nodes = base[:nb].view(NODE_DT)
         edges = base[nb:nb + eb].view(EDGE_DT)
-        rows = base[nb + eb:].reshape(self.node_cap, L.GAME_BYTES)
+        ro = (nb + eb + 15) // 16 * 16                # rows start 16-byte aligned (cit_cfr.h cfr_rows_offset)
+        rows = base[ro:ro + self.node_cap * L.GAME_BYTES].reshape(self.node_cap, L.GAME_BYTES)
         return nodes, edges, rows
 
     # --- single-game pieces of the search, exposed for the object API -------------

@@ -139,9 +139,10 @@ int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1,
 /* --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------ */
 
 /* Bytes of node pool per tree (64-bit: a cfr_train(200000) tree needs ~1 GB):
- * node_cap CfrNode (168 B) + edge_cap CfrEdge (48 B) + node_cap packed game
- * rows.  Opponent nodes reserve 10 edges, role-pick nodes 40 slots (10 edges +
- * their [6]-wide regret / strategy columns).  -1 on a bad capacity. */
+ * node_cap CfrNode (168 B) + edge_cap CfrEdge (48 B), padded to 16 B, +
+ * node_cap packed game rows (16-byte aligned).  Opponent nodes reserve 10
+ * edges, role-pick nodes 40 slots (10 edges + their [6]-wide regret /
+ * strategy columns).  -1 on a bad capacity. */
 int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap);
 int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */
 

@@ -88,8 +88,12 @@ WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])
 assert NODE_DT.itemsize == 168 and EDGE_DT.itemsize == 48 and WIDE_DT.itemsize == 3 * 48
 
 
+def cfr_rows_offset(node_cap, edge_cap):
+    return (node_cap * 168 + edge_cap * 48 + 15) // 16 * 16
+
+
 def cfr_pool_bytes(node_cap, edge_cap):
-    return node_cap * 168 + edge_cap * 48 + node_cap * L.GAME_BYTES
+    return cfr_rows_offset(node_cap, edge_cap) + node_cap * L.GAME_BYTES
 
 
 def node_arrays(nodes, edges, n):
@@ -141,7 +145,8 @@ class HostCfr:
         nb, eb = self.node_cap * 168, self.edge_cap * 48
         nodes = base[:nb].view(NODE_DT)
         edges = base[nb:nb + eb].view(EDGE_DT)
-        rows = base[nb + eb:].reshape(self.node_cap, L.GAME_BYTES)
+        ro = cfr_rows_offset(self.node_cap, self.edge_cap)
+        rows = base[ro:ro + self.node_cap * L.GAME_BYTES].reshape(self.node_cap, L.GAME_BYTES)
         return nodes, edges, rows
 
 

@@ -38,7 +38,8 @@ def test_layout_matches(lib):
 def test_cfr_pool_bytes_64bit(lib):
     # cfr_train(200000) pools exceed 2 GiB per tree (round 1 returned -1 there)
     nc, ec = 500_256, 5 * 500_256
-    assert lib.cit_cfr_pool_bytes(nc, ec) == nc * 168 + ec * 48 + nc * L.GAME_BYTES
+    assert lib.cit_cfr_pool_bytes(nc, ec) == (nc * 168 + ec * 48 + 15) // 16 * 16 + nc * L.GAME_BYTES
+    assert lib.cit_cfr_pool_bytes(3, 5) % 16 == 0   # rows (and the next tree's pool) 16-byte aligned
     assert lib.cit_cfr_pool_bytes(4_000_000, 20_000_000) > 2 ** 31
     assert lib.cit_cfr_pool_bytes(0, 10) == -1
 

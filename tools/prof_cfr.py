@@ -1,15 +1,23 @@
 """MCCFR phase-cycle breakdown (SURVEY §8(d) CFR row) on the GPU box.
 
-Builds (here, on the CPU: `python tools/prof_cfr.py build`) a variant of
-libcitadels_hip.so whose search translation unit is compiled with -DCIT_PROF
-(per-function clock64 accounting by lane 0 of each tree, csrc/cit_cfr.h
-CIT_PROF_SCOPE) into build/cfrprof/; on the box `python tools/prof_cfr.py run`
-runs config 3 (1024 positions, cfr_train(200)) and config 5 trees
-(cfr_train(2000)), and prints one JSON line per workload: calls, cycles per
-call and share of the search's cycles per phase.  Nested scopes: cfr_node
-contains skip-carry/prepare/list; expand_* contain copy_row, sample, carry,
-cfr_node; shares are of the top-level sum (expand_*, update_strategy, choose,
-backprop, live_choice)."""
+`python tools/prof_cfr.py build` (here, on the CPU) compiles variants of
+libcitadels_hip.so whose search translation unit has -DCIT_PROF (per-scope
+clock64 accounting by lane 0 of each tree, csrc/cit_cfr.h CIT_PROF_SCOPE),
+each timing only the scopes of one CIT_PROF_MASK, so that a variant's
+accounting perturbs the search little (one s_memtime pair per timed scope):
+
+  top    expand_role / expand_own / expand_opp / update_strategy / choose /
+         backprop / live_choice  (once per search iteration)
+  node   sample / copy_row / cfr_node
+  engine carry / prepare / list (LDS) / pick / list (HBM)
+
+`python tools/prof_cfr.py run` (GPU box) runs config 3 (1024 positions,
+cfr_train(200)) and config-5-style trees (cfr_train(2000)) with the plain
+library and with each variant, and prints one JSON line per (variant,
+workload): kernel ms (plain and profiled: the perturbation), calls, cycles per
+call, and each scope's share of the tree's cycles (scopes nest: cfr_node
+contains carry/prepare/list; expand_* contain copy_row, sample, carry,
+cfr_node)."""
 import ctypes as C
 import json
 import os
@@ -21,63 +29,77 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build", "cfrprof")
-LIB = os.path.join(OUT, "libcitprof.so")
-NAMES = ["carry", "prepare", "count", "pick", "list", "sample", "copy_row", "cfr_node", "exp_role", "exp_own",
+NAMES = ["carry", "prepare", "list_lds", "pick", "list", "sample", "copy_row", "cfr_node", "exp_role", "exp_own",
          "exp_opp", "upd_strategy", "choose", "upd_regrets", "backprop", "live_choice"]
+VARIANTS = {"top": (8, 9, 10, 11, 12, 14, 15), "node": (5, 6, 7), "engine": (0, 1, 2, 3, 4)}
+
+
+def lib_of(name):
+    return os.path.join(OUT, "libcitprof_%s.so" % name)
 
 
 def build():
     import __graft_entry__ as G
     os.makedirs(OUT, exist_ok=True)
-    objs = []
-    for u in G.HIP_UNITS:
-        o = os.path.join(OUT, u.replace(".hip", ".o"))
-        extra = ["-DCIT_PROF"] if u == "cit_cfr.hip" else []
-        if u != "cit_cfr.hip":
-            o = os.path.join(ROOT, "build", "hip", u.replace(".hip", ".o"))
-        else:
-            subprocess.check_call([G.HIPCC] + G.HIP_FLAGS + extra + ["-c", os.path.join(G.CSRC, u), "-o", o])
-        objs.append(o)
-    subprocess.check_call([G.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", LIB])
-    print(LIB)
+    others = [os.path.join(ROOT, "build", "hip", u.replace(".hip", ".o")) for u in G.HIP_UNITS if u != "cit_cfr.hip"]
+    for name, ids in VARIANTS.items():
+        mask = sum(1 << i for i in ids)
+        o = os.path.join(OUT, "cit_cfr_%s.o" % name)
+        subprocess.check_call([G.HIPCC] + G.HIP_FLAGS + ["-DCIT_PROF", "-DCIT_PROF_MASK=%d" % mask, "-c",
+                                                          os.path.join(G.CSRC, "cit_cfr.hip"), "-o", o])
+        subprocess.check_call([G.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", o] + others + ["-o", lib_of(name)])
+        print(lib_of(name))
 
 
-def run():
+def _workload(GameBatch, pool_caps, torch, B, iters):
+    b = GameBatch(np.arange(20_000_000, 20_000_000 + B), preset=True)
+    if iters == 200:
+        b.advance_random(0, 300)
+    else:
+        b.random_position(100)
+    b.seed_numpy()
+    torch.cuda.synchronize()
+    nc, ec = pool_caps(iters)
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    chosen, stats = b._cfr_decide(iters, nc, ec)
+    t1.record()
+    torch.cuda.synchronize()
+    return t0.elapsed_time(t1), stats.cpu().numpy()
+
+
+def run(which=None):
     import torch
     import citadels_self_play_amd._lib as LL
-    LL.LIB_PATH = LIB
-    from citadels_self_play_amd import _lib
     from citadels_self_play_amd.engine import GameBatch, pool_caps
-    lib = _lib.load()
-    lib.cit_prof_read.argtypes = [C.c_void_p]
-    buf = (C.c_ulonglong * 32)()
-    for tag, B, iters in (("config3", 1024, 200), ("config5_2000", 1024, 2000)):
-        b = GameBatch(np.arange(20_000_000, 20_000_000 + B), preset=True)
-        if iters == 200:
-            b.advance_random(0, 300)
-        else:
-            b.random_position(100)
-        b.seed_numpy()
-        torch.cuda.synchronize()
-        lib.cit_prof_read(buf)
-        nc, ec = pool_caps(iters)
-        t0 = torch.cuda.Event(enable_timing=True)
-        t1 = torch.cuda.Event(enable_timing=True)
-        t0.record()
-        chosen, stats = b.cfr_decide(iters, node_cap=nc, edge_cap=ec)
-        t1.record()
-        torch.cuda.synchronize()
-        lib.cit_prof_read(buf)
-        v = np.array(list(buf), dtype=np.float64)
-        cyc, cnt = v[:16], v[16:]
-        st = stats.cpu().numpy()
-        top = cyc[[8, 9, 10, 11, 12, 14, 15]].sum()      # the top-level scopes of the search loop
-        phases = {n: {"calls": int(cnt[i]), "cycles_per_call": cyc[i] / max(cnt[i], 1),
-                      "share_of_search": cyc[i] / top} for i, n in enumerate(NAMES)}
-        print(json.dumps({"workload": tag, "trees": B, "iters": iters, "ms": t0.elapsed_time(t1),
-                          "carry_outs": int(st[:, 3].sum()), "nodes": int(st[:, 1].sum()),
-                          "cycles_per_tree": top / B, "phases": phases}), flush=True)
+    loads = [("plain", LL.LIB_PATH)] + [(n, lib_of(n)) for n in VARIANTS if which in (None, n)]
+    plain = {}
+    for vname, path in loads:
+        LL._lib = None
+        LL.LIB_PATH = path
+        lib = LL.load()
+        if vname != "plain":
+            lib.cit_prof_read.argtypes = [C.c_void_p]
+            buf = (C.c_ulonglong * 32)()
+        for tag, B, iters in (("config3", 1024, 200), ("config5_2000", 1024, 2000)):
+            if vname != "plain":
+                lib.cit_prof_read(buf)
+            ms, st = _workload(GameBatch, pool_caps, torch, B, iters)
+            if vname == "plain":
+                plain[tag] = ms
+                continue
+            lib.cit_prof_read(buf)
+            v = np.array(list(buf), dtype=np.float64)
+            cyc, cnt = v[:16], v[16:]
+            ids = VARIANTS[vname]
+            phases = {NAMES[i]: {"calls": int(cnt[i]), "cycles_per_call": cyc[i] / max(cnt[i], 1),
+                                 "cycles_per_tree": cyc[i] / B, "cycles_per_carry": cyc[i] / max(st[:, 3].sum(), 1)}
+                      for i in ids}
+            print(json.dumps({"variant": vname, "workload": tag, "trees": B, "iters": iters, "ms": ms,
+                              "ms_plain": plain.get(tag), "carry_outs": int(st[:, 3].sum()),
+                              "nodes": int(st[:, 1].sum()), "phases": phases}), flush=True)
 
 
 if __name__ == "__main__":
-    build() if sys.argv[1:] == ["build"] else run()
+    build() if sys.argv[1:] == ["build"] else run(*sys.argv[2:])

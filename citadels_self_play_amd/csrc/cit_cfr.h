@@ -216,55 +216,6 @@ CIT_HD uint32_t* w_row(const CfrTree& T, int which) { return reinterpret_cast<ui
 #define CIT_NOINLINE inline
 #endif
 
-// Optional per-function cycle accounting (build with -DCIT_PROF; profiling
-// only, tools/prof_cfr.py).  Each tree accumulates its scopes' cycles in LDS
-// (one wave per tree: plain adds by lane 0, no atomics inside the search, so
-// the accounting does not perturb the memory traffic it measures); the
-// kernel adds the totals to g_cit_prof once per tree (cfr_prof_flush).
-// Scopes nest: a scope's cycles include those of the scopes it calls.
-#if defined(CIT_PROF) && defined(__HIPCC__)
-__device__ unsigned long long g_cit_prof[32];
-#endif
-#if defined(CIT_PROF) && defined(__HIP_DEVICE_COMPILE__)
-__shared__ unsigned long long cit_prof_lds[32];
-struct CitProf {
-  int id;
-  unsigned long long t0;
-  __device__ explicit CitProf(int i) : id(i), t0(clock64()) {}
-  __device__ ~CitProf() {
-    unsigned long long dt = clock64() - t0;
-    if (threadIdx.x == 0) {
-      cit_prof_lds[id] += dt;
-      cit_prof_lds[16 + id] += 1ull;
-    }
-  }
-};
-// CIT_PROF_MASK selects the scopes that are timed (bit i = scope i), so a
-// profile can time a few scopes at a time with little perturbation.
-#ifndef CIT_PROF_MASK
-#define CIT_PROF_MASK 0xffff
-#endif
-struct CitProfOff {
-  __device__ explicit CitProfOff(int) {}
-};
-#define CIT_PROF_SCOPE(i)                                                         \
-  typename cit_prof_sel<((CIT_PROF_MASK >> (i)) & 1) != 0>::type _cit_prof_scope(i)
-template <bool On> struct cit_prof_sel { typedef CitProf type; };
-template <> struct cit_prof_sel<false> { typedef CitProfOff type; };
-__device__ inline void cfr_prof_reset() {
-  if (threadIdx.x < 32) cit_prof_lds[threadIdx.x] = 0;
-  __syncthreads();
-}
-__device__ inline void cfr_prof_flush() {
-  __syncthreads();
-  if (threadIdx.x < 32) atomicAdd(&g_cit_prof[threadIdx.x], cit_prof_lds[threadIdx.x]);
-}
-#else
-#define CIT_PROF_SCOPE(i) ((void)0)
-#define cfr_prof_reset() ((void)0)
-#define cfr_prof_flush() ((void)0)
-#endif
-
 // option.carry_out on working row `which`, counted; returns the winner (-1: none)
 CIT_NOINLINE int eng_carry(CfrTree& T_in, int which, CitOpt o_in) {
   CIT_PROF_SCOPE(0);

@@ -190,8 +190,8 @@ int cit_tree_clock_read(unsigned long long* out, int n) {
 
 #if defined(CIT_PROF)
 int cit_prof_read(unsigned long long* out) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cit_prof), sizeof(unsigned long long) * 32);
-  unsigned long long z[32] = {0};
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cit_prof), sizeof(unsigned long long) * 64);
+  unsigned long long z[64] = {0};
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_cit_prof), z, sizeof(z));
   return (int)e;
 }

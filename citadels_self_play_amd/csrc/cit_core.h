@@ -202,6 +202,56 @@ enum { WB_NONE = 0, WB_REAL = 1, WB_FAKE = 2 };
 static_assert(sizeof(CitGame) <= CIT_GAME_BYTES, "CitGame grew past its row size");
 static_assert(CIT_GAME_BYTES % 16 == 0, "row must be 16-byte aligned");
 
+// Optional per-function cycle accounting (build with -DCIT_PROF; profiling
+// only, tools/prof_cfr.py; scopes 0..15: the search in cit_cfr.h, 16..31:
+// engine internals).  Each tree accumulates its scopes' cycles in LDS
+// (one wave per tree: plain adds by lane 0, no atomics inside the search, so
+// the accounting does not perturb the memory traffic it measures); the
+// kernel adds the totals to g_cit_prof once per tree (cfr_prof_flush).
+// Scopes nest: a scope's cycles include those of the scopes it calls.
+#if defined(CIT_PROF) && defined(__HIPCC__)
+__device__ unsigned long long g_cit_prof[64];
+#endif
+#if defined(CIT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+__shared__ unsigned long long cit_prof_lds[64];
+struct CitProf {
+  int id;
+  unsigned long long t0;
+  __device__ explicit CitProf(int i) : id(i), t0(clock64()) {}
+  __device__ ~CitProf() {
+    unsigned long long dt = clock64() - t0;
+    if (threadIdx.x == 0) {
+      cit_prof_lds[id] += dt;
+      cit_prof_lds[32 + id] += 1ull;
+    }
+  }
+};
+// CIT_PROF_MASK selects the scopes that are timed (bit i = scope i), so a
+// profile can time a few scopes at a time with little perturbation.
+#ifndef CIT_PROF_MASK
+#define CIT_PROF_MASK 0xffffffffull
+#endif
+struct CitProfOff {
+  __device__ explicit CitProfOff(int) {}
+};
+#define CIT_PROF_SCOPE(i)                                                         \
+  typename cit_prof_sel<((CIT_PROF_MASK >> (i)) & 1ull) != 0>::type _cit_prof_scope(i)
+template <bool On> struct cit_prof_sel { typedef CitProf type; };
+template <> struct cit_prof_sel<false> { typedef CitProfOff type; };
+__device__ inline void cfr_prof_reset() {
+  cit_prof_lds[threadIdx.x] = 0;   // 64 lanes, 64 slots
+  __syncthreads();
+}
+__device__ inline void cfr_prof_flush() {
+  __syncthreads();
+  atomicAdd(&g_cit_prof[threadIdx.x], cit_prof_lds[threadIdx.x]);
+}
+#else
+#define CIT_PROF_SCOPE(i) ((void)0)
+#define cfr_prof_reset() ((void)0)
+#define cfr_prof_flush() ((void)0)
+#endif
+
 // ----------------------------------------------------------------- MT19937
 // Per-lane MT19937 laid out structure-of-arrays: word i of lane l at
 // mt[i*stride + l].  The stream position lives in a register while a kernel

@@ -180,31 +180,23 @@ CIT_HD int deck_take_like(CitGame& g, int c) {
   }
   return c;
 }
-// random.shuffle (Lib/random.py:380-392) over any indexable sequence.
-// Wave path (a coop LDS stream, n <= 128, a sequence in shared memory; a
-// lane-private array keeps the serial loop): the sequence moves into two VGPRs
-// (lane i holds elements i and 64 + i), the draws come through a register
-// window and each swap is two readlanes and two writelanes, so the serial
-// chain has no memory round trip; the lanes store the result back.
+// random.shuffle (Lib/random.py:380-392) over any indexable sequence.  With
+// a coop (LDS) stream under CIT_WAVE the draws come through a register
+// window (a readlane each instead of an LDS round trip per draw); the swaps
+// stay serial (LDS operations of one wave are in order, so a swap's reads
+// never wait on the previous swap's writes).
 template <class At>
 CIT_HD void shuffle_seq(CitMT& rng, int n, At at) {
 #if CIT_WAVE
-  if (n <= 128 && rng.coop && !__builtin_amdgcn_is_private((const void*)&at(0))) {
-    const int l = cit_lane();
-    int v0 = l < n ? at(l) : 0, v1 = l + 64 < n ? at(l + 64) : 0;
+  if (rng.coop && n > 1) {
     CitMT w = cit_mt_window(rng);
     for (int i = n - 1; i > 0; i--) {
       int j = (int)mt_randbelow(w, (uint32_t)(i + 1));
-      int ai = i < 64 ? cit_readlane(v0, i) : cit_readlane(v1, i - 64);
-      int aj = j < 64 ? cit_readlane(v0, j) : cit_readlane(v1, j - 64);
-      if (i < 64) v0 = cit_writelane(v0, aj, i);
-      else v1 = cit_writelane(v1, aj, i - 64);
-      if (j < 64) v0 = cit_writelane(v0, ai, j);
-      else v1 = cit_writelane(v1, ai, j - 64);
+      uint8_t t = at(i);
+      at(i) = at(j);
+      at(j) = t;
     }
     cit_mt_unwindow(rng, w);
-    if (l < n) at(l) = (uint8_t)v0;
-    if (l + 64 < n) at(l + 64) = (uint8_t)v1;
     return;
   }
 #endif
@@ -1906,7 +1898,7 @@ CIT_HD void kr_strip(const CitGame& g, uint16_t* kr, int role) {
   }
 }
 
-#define CIT_SAMPLE_SCRATCH 256   // bytes of `unk` scratch cit_sample_private needs
+#define CIT_SAMPLE_SCRATCH 1024   // bytes of `unk` scratch cit_sample_private needs
 
 #if CIT_WAVE
 // Append src(i), i < cnt (<= 128), to dst[base..) skipping CIT_NO_CARD (the
@@ -1927,7 +1919,8 @@ CIT_HD int wave_append(Dst dst, int base, int cnt, Src src) {
 // cit_sample_private for a wave running the game uniformly with a coop (LDS)
 // stream: the same draws in the same order (through a register window), the
 // list work spread over the lanes.  `unk` holds >= CIT_SAMPLE_SCRATCH bytes:
-// the unknown cards [0, 80) and the per-type removal counts u32[40] at 80.
+// the unknown cards [0, 80), the per-type removal counts u32[40] at 80 and
+// the per-type lane masks of the used cards u64[2][40] at 240.
 CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitMT& rng, uint8_t* unk) {
   const int l = cit_lane();
   const uint64_t below = cit_below();
@@ -1943,18 +1936,29 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
   const bool mine = l < nkh && kowner == orig;
   // hk.used with probability (confidence-1)*0.2, entries in order (:217-222)
   uint64_t used = 0;
+  {
+  CIT_PROF_SCOPE(16);
   for (uint64_t m = cit_ballot(mine); m; m &= m - 1) {
     int e = __ffsll((unsigned long long)m) - 1;
     double r = mt_random(w);
     int conf = cit_readlane(kflags, e) & 15;
     if ((double)(conf - 1) * 0.2 > r) used |= 1ull << e;
   }
+  }
   const bool uu = mine && ((used >> l) & 1);
   if (mine) g.kh[l].conf_flags = (uint8_t)((kflags & ~0x20) | (uu ? 0x20 : 0));
   // get_unknown_cards (:183-213): removals per type, then drop the first k_t
   // used cards of each type t
+  int nu = 0;
+  {
+  CIT_PROF_SCOPE(17);
   uint32_t* kt = reinterpret_cast<uint32_t*>(unk + CIT_USED_CAP);
-  if (l < 40) kt[l] = 0;
+  uint64_t* tm = reinterpret_cast<uint64_t*>(unk + CIT_USED_CAP + 160);   // [2][40]
+  if (l < 40) {
+    kt[l] = 0;
+    tm[l] = 0;
+    tm[40 + l] = 0;
+  }
   __syncthreads();
   for (int pass = 0; pass < 2; pass++) {
     int p = pass * 4 + (l >> 4), i = l & 15;
@@ -1974,29 +1978,26 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
   const bool v0 = l < nuc, v1 = l + 64 < nuc;
   const int c0 = v0 ? g.used_cards[l] : 0, c1 = v1 ? g.used_cards[l + 64] : 0;
   const int t0 = card_type(c0), t1 = card_type(c1);
-  int rk0 = 0, rk1 = 0;                          // rank among the earlier used cards of the same type
-  uint64_t rem0 = cit_ballot(v0), rem1 = cit_ballot(v1);
-  while (rem0 | rem1) {
-    int t = rem0 ? cit_readlane(t0, __ffsll((unsigned long long)rem0) - 1)
-                 : cit_readlane(t1, __ffsll((unsigned long long)rem1) - 1);
-    uint64_t m0 = cit_ballot(v0 && t0 == t), m1 = cit_ballot(v1 && t1 == t);
-    if (t0 == t) rk0 = __popcll(m0 & below);
-    if (t1 == t) rk1 = __popcll(m0) + __popcll(m1 & below);
-    rem0 &= ~m0;
-    rem1 &= ~m1;
-  }
+  // rank among the earlier used cards of the same type: per-type masks of
+  // the lanes holding that type (LDS atomic OR), popcount below this lane
+  if (v0) atomicOr(reinterpret_cast<unsigned long long*>(&tm[t0]), 1ull << l);
+  if (v1) atomicOr(reinterpret_cast<unsigned long long*>(&tm[40 + t1]), 1ull << l);
+  __syncthreads();
+  const int rk0 = __popcll(tm[t0] & below), rk1 = __popcll(tm[t1]) + __popcll(tm[40 + t1] & below);
   const bool k0 = v0 && rk0 >= (int)kt[t0], k1 = v1 && rk1 >= (int)kt[t1];
   const uint64_t km0 = cit_ballot(k0), km1 = cit_ballot(k1);
   const int nk0 = __popcll(km0);
   __syncthreads();
   if (k0) unk[__popcll(km0 & below)] = (uint8_t)c0;
   if (k1) unk[nk0 + __popcll(km1 & below)] = (uint8_t)c1;
-  const int nu = nk0 + __popcll(km1);
+  nu = nk0 + __popcll(km1);
   __syncthreads();
+  }
   int head = 0;                                  // unk[head..nu): the undealt unknown cards
   auto deck_slot = [&g](int i) -> uint8_t& { return g.deck[i & (CIT_DECK_CAP - 1)]; };
   // sample_deck (:245-262): lighthouse knowledge first, then shuffled unknowns
   {
+    CIT_PROF_SCOPE(18);
     int n = g.n_deck, nd = 0;
     uint64_t lm = cit_ballot(uu && ktarget == -1);
     g.n_deck = 0;
@@ -2018,6 +2019,7 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
   // sample_warrants_and_blackmails (:321-336): the marked roles (<= 8) as
   // nibbles of one word, shuffled; the first is the real one
   for (int which = 0; which < 2; which++) {
+    CIT_PROF_SCOPE(19);
     int shift = which == 0 ? RP_BLACKMAIL_SHIFT : RP_WARRANT_SHIFT;
     uint32_t pk = 0;
     int nk = 0;
@@ -2036,15 +2038,23 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
       g.rp[r] = (uint8_t)((g.rp[r] & ~(3u << shift)) | ((r == real ? WB_REAL : WB_FAKE) << shift));
     }
   }
+  CIT_PROF_SCOPE(20);
   uint16_t kr[CIT_NP];
   for (int j = 0; j < CIT_NP; j++) kr[j] = PC.kr[j];
+  // kr_strip: the role ids holding `role` as one ballot over lane r = roles[r]
+  const int rl = l < 8 ? g.roles[l] : ROLE_NONE;
+  auto strip = [&](int role) {
+    uint16_t m = (uint16_t)(((uint32_t)cit_ballot(l < 8 && rl == role) << 1) | (role == ROLE_BEWITCHED ? 1u : 0u));
+    for (int j = 0; j < CIT_NP; j++)
+      if (!(kr[j] & KR_CONFIRMED)) kr[j] &= (uint16_t)~m;
+  };
   if (role_sample) {   // remove_role_and_smaller_id_roles_from_role_knowledge_if_unconfirmed (:304-310)
     int role = g.pl[g.gs_pid].role;
-    kr_strip(g, kr, role);
+    strip(role);
     if (role != ROLE_NONE) {
       int rr = role_rank(g, role);
       for (int rid = 0; rid < 8; rid++)
-        if (rid < rr) kr_strip(g, kr, g.roles[rid]);
+        if (rid < rr) strip(cit_readlane(rl, rid));
     }
   }
   for (int p = 0; p < CIT_NP; p++) {
@@ -2078,8 +2088,8 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
             if (k == 0) { rid = q; break; }
             k--;
           }
-        Q.role = (uint8_t)role_of_id(g, rid);
-        kr_strip(g, kr, Q.role);
+        Q.role = (uint8_t)(rid < 0 ? ROLE_BEWITCHED : cit_readlane(rl, rid));
+        strip(Q.role);
       } else {   // the IndexError band-aid: first role id not in used_roles
         int pick = -1;
         for (int rid = 0; rid < 8 && pick < 0; rid++) {

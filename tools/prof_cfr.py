@@ -10,6 +10,7 @@ accounting perturbs the search little (one s_memtime pair per timed scope):
          backprop / live_choice  (once per search iteration)
   node   sample / copy_row / cfr_node
   engine carry / prepare / list (LDS) / pick / list (HBM)
+  sample the determinization's parts (cit_engine.h cit_sample_private_wave)
 
 `python tools/prof_cfr.py run` (GPU box) runs config 3 (1024 positions,
 cfr_train(200)) and config-5-style trees (cfr_train(2000)) with the plain
@@ -30,8 +31,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build", "cfrprof")
 NAMES = ["carry", "prepare", "list_lds", "pick", "list", "sample", "copy_row", "cfr_node", "exp_role", "exp_own",
-         "exp_opp", "upd_strategy", "choose", "upd_regrets", "backprop", "live_choice"]
-VARIANTS = {"top": (8, 9, 10, 11, 12, 14, 15), "node": (5, 6, 7), "engine": (0, 1, 2, 3, 4)}
+         "exp_opp", "upd_strategy", "choose", "upd_regrets", "backprop", "live_choice",
+         "smp_used", "smp_unknown", "smp_deck", "smp_warrants", "smp_opponents"] + ["s%d" % i for i in range(21, 32)]
+VARIANTS = {"top": (8, 9, 10, 11, 12, 14, 15), "node": (5, 6, 7), "engine": (0, 1, 2, 3, 4),
+            "sample": (5, 16, 17, 18, 19, 20)}
 
 
 def lib_of(name):
@@ -45,7 +48,7 @@ def build():
     for name, ids in VARIANTS.items():
         mask = sum(1 << i for i in ids)
         o = os.path.join(OUT, "cit_cfr_%s.o" % name)
-        subprocess.check_call([G.HIPCC] + G.HIP_FLAGS + ["-DCIT_PROF", "-DCIT_PROF_MASK=%d" % mask, "-c",
+        subprocess.check_call([G.HIPCC] + G.HIP_FLAGS + ["-DCIT_PROF", "-DCIT_PROF_MASK=%dull" % mask, "-c",
                                                           os.path.join(G.CSRC, "cit_cfr.hip"), "-o", o])
         subprocess.check_call([G.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", o] + others + ["-o", lib_of(name)])
         print(lib_of(name))
@@ -81,7 +84,7 @@ def run(which=None):
         lib = LL.load()
         if vname != "plain":
             lib.cit_prof_read.argtypes = [C.c_void_p]
-            buf = (C.c_ulonglong * 32)()
+            buf = (C.c_ulonglong * 64)()
         for tag, B, iters in (("config3", 1024, 200), ("config5_2000", 1024, 2000)):
             if vname != "plain":
                 lib.cit_prof_read(buf)
@@ -91,7 +94,7 @@ def run(which=None):
                 continue
             lib.cit_prof_read(buf)
             v = np.array(list(buf), dtype=np.float64)
-            cyc, cnt = v[:16], v[16:]
+            cyc, cnt = v[:32], v[32:]
             ids = VARIANTS[vname]
             phases = {NAMES[i]: {"calls": int(cnt[i]), "cycles_per_call": cyc[i] / max(cnt[i], 1),
                                  "cycles_per_tree": cyc[i] / B, "cycles_per_carry": cyc[i] / max(st[:, 3].sum(), 1)}

@@ -103,9 +103,11 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
 
     Node pools are sized from `iters` (engine.pool_caps: a cfr_train(200000)
     tree takes ~0.5-1 GB); when the seeds' pools do not fit in
-    `max_pool_bytes` (default: 60 % of the free device memory) the seeds run in
-    consecutive chunks and the results are concatenated in seed order (the
-    returned batch is then the last chunk's)."""
+    `max_pool_bytes` (default: 80 % of the device memory not held by live
+    tensors) the seeds run in consecutive equal chunks and the results are
+    concatenated in seed order (the returned batch is then the last chunk's).
+    targets["terminal"] [B] marks the positions that were already over (the
+    reference's run_mccfr raises ValueError on them)."""
     from . import _lib
     if node_cap is None:
         node_cap, ec = pool_caps(iters)
@@ -114,9 +116,12 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
     dev = torch.device(device or "cuda")
     per = _lib.load().cit_cfr_pool_bytes(node_cap, edge_cap)
     if max_pool_bytes is None:
-        max_pool_bytes = int(0.6 * torch.cuda.mem_get_info(dev)[0])
+        torch.cuda.empty_cache()                # cached blocks of earlier pools count as free
+        max_pool_bytes = int(0.8 * torch.cuda.mem_get_info(dev)[0])
     seeds = np.asarray(seeds, np.int64)
     chunk = int(max(1, min(len(seeds), max_pool_bytes // max(per, 1))))
+    n_chunks = -(-len(seeds) // chunk)
+    chunk = -(-len(seeds) // n_chunks)           # equal chunks: no short last launch
     parts = []
     b = None
     for i in range(0, len(seeds), chunk):
@@ -125,8 +130,11 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
         b = GameBatch(seeds[i:i + chunk], preset=True, device=dev)
         b.random_position(max_move)
         b.seed_numpy()
+        term = b.terminal()
         chosen, stats = b.cfr_decide(iters, node_cap=node_cap, edge_cap=edge_cap)
-        parts.append((stats, b.cfr_targets(stats[:, 0], mode=0)))
+        t = b.cfr_targets(stats[:, 0], mode=0)
+        t["terminal"] = term
+        parts.append((stats, t))
         if log is not None and len(seeds) > chunk:
             log("simulate_games: trees %d-%d of %d done" % (i, i + b.B - 1, len(seeds)))
     if len(parts) == 1:
@@ -147,8 +155,9 @@ def concat_targets(ts, sizes):
         lane0 += n
         row0 += t["dist"].shape[0]
     out = {"meta": torch.cat(metas)}
-    for k in ("feat", "value", "dist", "opt_feat", "counts"):
-        out[k] = torch.cat([t[k] for t in ts])
+    for k in ("feat", "value", "dist", "opt_feat", "counts", "terminal"):
+        if all(k in t for t in ts):
+            out[k] = torch.cat([t[k] for t in ts])
     return out
 
 

@@ -77,9 +77,8 @@ def main():
                                                   log=(lambda m: print(m, file=sys.stderr, flush=True)))
             f, v = selfplay.all_gather_targets(t["feat"], t["value"])
             n_targets = int(f.shape[0])
-            # k = 1 picks the final (terminal) game: ValueError in the reference (known only for one chunk)
-            term = b.terminal() if b.B == stats.shape[0] else torch.zeros(stats.shape[0], dtype=torch.bool,
-                                                                            device=dev)
+            # k = 1 picks the final (terminal) game: ValueError in the reference
+            term = t["terminal"]
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

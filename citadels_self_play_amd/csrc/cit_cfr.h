@@ -449,7 +449,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   bool done = false;
   while (n == 1 && !done && !e && !w.err) {
     i++;
-    CitOpt o = cfr_lbuf(T)[0];
+    CitOpt o = cfr_uopt(cfr_lbuf(T)[0]);
     int win = cfr_u(eng_carry(T, which, o));
     done = win >= 0;
     eng_prepare(T, which);
@@ -531,7 +531,7 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
       T.err |= c.err;
       int k = np_choice_uniform(T.np, c.n, T.err);
       if (T.err) break;
-      last = k < CFR_LBUF ? cfr_lbuf(T)[k] : cfr_uopt(eng_pick(T, 1, k));
+      last = k < CFR_LBUF ? cfr_uopt(cfr_lbuf(T)[k]) : cfr_uopt(eng_pick(T, 1, k));
       eng_carry(T, 1, last);
       T.err |= h.err;
       if (++guard > 64) T.err |= CIT_ERR_UNSUPPORTED;
@@ -602,7 +602,7 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
   T.err |= lc.err | h.err;
   int k = np_choice_uniform(T.np, lc.n, T.err);
   if (T.err) return;
-  CitOpt o = k < CFR_LBUF ? cfr_lbuf(T)[k] : cfr_uopt(eng_pick(T, 1, k));
+  CitOpt o = k < CFR_LBUF ? cfr_uopt(cfr_lbuf(T)[k]) : cfr_uopt(eng_pick(T, 1, k));
   opt_mutate(o, h);
   CitOpt key = opt_key(o, h);
   eng_carry(T, 1, o);

@@ -170,6 +170,22 @@ CIT_HD void deck_put(CitGame& g, int c) {
 }
 CIT_HD int deck_take_like(CitGame& g, int c) {
   int t = card_type(c);
+#if CIT_WAVE
+  {   // lanes l / 64 + l hold logical positions l / 64 + l; one ballot finds the
+      // first match, every lane loads before any lane stores the shifted tail
+    const int nd = g.n_deck, head = g.deck_head, l = cit_lane();
+    int c0 = l < nd ? g.deck[(head + l) & (CIT_DECK_CAP - 1)] : CIT_NO_CARD;
+    int c1 = l + 64 < nd ? g.deck[(head + l + 64) & (CIT_DECK_CAP - 1)] : CIT_NO_CARD;
+    uint64_t m0 = cit_ballot(l < nd && card_type(c0) == t), m1 = cit_ballot(l + 64 < nd && card_type(c1) == t);
+    if (!(m0 | m1)) return c;
+    int i = m0 ? __ffsll((unsigned long long)m0) - 1 : 64 + __ffsll((unsigned long long)m1) - 1;
+    int r = i < 64 ? cit_readlane(c0, i) : cit_readlane(c1, i - 64);
+    if (l > i && l < nd) g.deck[(head + l - 1) & (CIT_DECK_CAP - 1)] = (uint8_t)c0;
+    if (l + 64 > i && l + 64 < nd) g.deck[(head + l + 63) & (CIT_DECK_CAP - 1)] = (uint8_t)c1;
+    g.n_deck = (uint8_t)(nd - 1);
+    return r;
+  }
+#endif
   for (int i = 0; i < g.n_deck; i++) {
     if (card_type(deck_at(g, i)) == t) {
       int r = deck_at(g, i);
@@ -500,18 +516,45 @@ CIT_HD void cit_setup_round(CitGame& g, CitMT& rng) {
 // Game(preset) + set_initial_variables + create_game's setup_round, for a
 // game whose CPython stream has just been seeded.
 CIT_HD void cit_init_game(CitGame& g, CitMT& rng, bool preset) {
-  uint8_t* z = (uint8_t*)&g;
-  for (int i = 0; i < (int)sizeof(CitGame); i++) z[i] = 0;
   // building_cards multiplicities per type 0..15, one nibble each (config.py:2-52)
   const uint64_t kBaseCounts = 0x3543333233324335ull;
   uint8_t uniq[24];
   for (int i = 0; i < 24; i++) uniq[i] = (uint8_t)(i == 0 ? 16 : i == 1 || i == 2 ? 17 : i < 23 ? i + 15 : 39);
   int n = 0;
+#if CIT_WAVE
+  {   // the row zeroed and the 52 base cards (+ the 24 uniques of the preset) laid out by the lanes
+    const int l = cit_lane();
+    static_assert(sizeof(CitGame) % 4 == 0, "row words");
+    for (int i = l; i < (int)(sizeof(CitGame) / 4); i += 64) reinterpret_cast<uint32_t*>(&g)[i] = 0;
+    int v0 = 0, v1 = 0, off = 0;
+    for (int k = 0; k < 16; k++) {
+      int cnt = (int)((kBaseCounts >> (4 * k)) & 15);
+      if (l >= off && l < off + cnt) v0 = k;
+      if (l + 64 >= off && l + 64 < off + cnt) v1 = k;
+      off += cnt;
+    }
+    n = off;                                        // 52
+    if (preset) {
+      int u = l - n;
+      if (u >= 0 && u < 24) v0 = u == 0 ? 16 : u == 1 || u == 2 ? 17 : u < 23 ? u + 15 : 39;
+      int u1 = l + 64 - n;
+      if (u1 >= 0 && u1 < 24) v1 = u1 == 0 ? 16 : u1 == 1 || u1 == 2 ? 17 : u1 < 23 ? u1 + 15 : 39;
+    }
+    int nn = preset ? n + 24 : n;
+    if (l < nn) g.deck[l] = (uint8_t)v0;
+    if (l + 64 < nn) g.deck[l + 64] = (uint8_t)v1;
+    n = nn;
+  }
+  if (!preset) {
+#else
+  uint8_t* z = (uint8_t*)&g;
+  for (int i = 0; i < (int)sizeof(CitGame); i++) z[i] = 0;
   for (int k = 0; k < 16; k++)
     for (int j = 0; j < (int)((kBaseCounts >> (4 * k)) & 15); j++) g.deck[n++] = (uint8_t)k;
   if (preset) {
     for (int i = 0; i < 24; i++) g.deck[n++] = uniq[i];
   } else {
+#endif
     // random.sample(unique_building_cards, 14): pool variant (Lib/random.py:483-490)
     uint8_t pool[24];
     for (int i = 0; i < 24; i++) pool[i] = uniq[i];
@@ -524,7 +567,16 @@ CIT_HD void cit_init_game(CitGame& g, CitMT& rng, bool preset) {
   g.deck_head = 0;
   g.n_deck = (uint8_t)n;
   deck_shuffle(g, rng);
+#if CIT_WAVE
+  {
+    const int l = cit_lane();
+    int d0 = l < n ? g.deck[l] : 0, d1 = l + 64 < n ? g.deck[l + 64] : 0;
+    if (l < n) g.used_cards[l] = (uint8_t)d0;
+    if (l + 64 < n && l + 64 < CIT_USED_CAP) g.used_cards[l + 64] = (uint8_t)d1;
+  }
+#else
   for (int i = 0; i < n; i++) g.used_cards[i] = g.deck[i];
+#endif
   g.n_used_cards = (uint8_t)n;
   for (int i = 0; i < CIT_NP; i++) {
     g.pl[i].gold = 2;

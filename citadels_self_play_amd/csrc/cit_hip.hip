@@ -78,6 +78,67 @@ __device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint
     for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) mt[(long)i * B + l] = mts[i];
 }
 
+// init_genrand(19650218), the first step of CPython's init_by_array, is the
+// same for every seed: a compile-time table.
+struct CitMTInitTable {
+  uint32_t w[CIT_MT_N];
+};
+constexpr CitMTInitTable cit_mt_init_table() {
+  CitMTInitTable t{};
+  uint32_t s = 19650218u;
+  t.w[0] = s;
+  for (int i = 1; i < CIT_MT_N; i++) {
+    s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i;
+    t.w[i] = s;
+  }
+  return t;
+}
+__constant__ CitMTInitTable c_mt_init = cit_mt_init_table();
+
+// CPython random.seed(int) (init_by_array) for 64 games per workgroup, one
+// game per lane: each game's recurrence is serial, so the parallelism is
+// across games.  The first pass reads the constant table, the second reads
+// the first pass's words back from LDS ([624][64], 156 KB: one workgroup per
+// CU); the words then go to HBM structure-of-arrays.  Same stream as
+// mt_seed_cpython (cit_core.h).
+__global__ __launch_bounds__(64) void k_mt_seed_cpython(uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds) {
+  __shared__ uint32_t m[CIT_MT_N * 64];
+  const int l = threadIdx.x;
+  const long g = (long)blockIdx.x * 64 + l;
+  const bool on = g < B;
+  const uint64_t seed = on ? seeds[g] : 0;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const int klen = k1 ? 2 : 1;
+  uint32_t prev = c_mt_init.w[0];
+  int j = 0;
+  // pass 1 (k = 624 steps): i = 1..623 read the table, the 624th (i = 1 again) its own output
+  for (int i = 1; i < CIT_MT_N; i++) {
+    uint32_t v = (c_mt_init.w[i] ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? k1 : k0) + (uint32_t)j;
+    m[i * 64 + l] = v;
+    prev = v;
+    j = j + 1 >= klen ? 0 : j + 1;
+  }
+  m[l] = prev;
+  {
+    uint32_t v = (m[64 + l] ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? k1 : k0) + (uint32_t)j;
+    m[64 + l] = v;
+    prev = v;
+  }
+  // pass 2 (623 steps): i = 2..623, then i = 1
+  for (int i = 2; i < CIT_MT_N; i++) {
+    uint32_t v = (m[i * 64 + l] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
+    m[i * 64 + l] = v;
+    prev = v;
+  }
+  m[l] = prev;
+  m[64 + l] = (m[64 + l] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - 1u;
+  m[l] = 0x80000000u;
+  if (on) {
+    for (int i = 0; i < CIT_MT_N; i++) mt[(long)i * B + g] = m[i * 64 + l];
+    idx[g] = CIT_MT_N;
+  }
+}
+
 __global__ void k_mt_seed(uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds, int numpy_style) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= B) return;
@@ -342,8 +403,13 @@ int cit_randbelow(uint32_t* mt, uint32_t* mt_idx, int B, int bound, int32_t* out
 int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int preset,
              hipStream_t stream) {
   if (B <= 0 || !games || !mt || !mt_idx) return -1;
+  if (seeds) {   // random.seed(s) for every lane (one game per lane), then the deal continues the streams
+    hipLaunchKernelGGL(k_mt_seed_cpython, dim3((B + 63) / 64), dim3(64), 0, stream, mt, mt_idx, B, seeds);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
   hipLaunchKernelGGL(k_init, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, B,
-                     seeds, preset);
+                     (const uint64_t*)nullptr, preset);
   CHECK_LAUNCH();
 }
 

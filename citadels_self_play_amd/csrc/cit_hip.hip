@@ -278,11 +278,20 @@ __device__ int prof_step(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* buf, in
 }
 #endif
 
+#ifdef ROLL_CLOCK
+// Per-game start / end wall clock (100 MHz) of k_rollout_u (measurement builds
+// only: tools/rollout_clock.py).
+__device__ unsigned long long g_roll_clock[2 * 65536];
+#endif
+
 // The hot loop (default): one game per workgroup (uniform_game), row and
 // MT19937 words in LDS for the whole rollout.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_rollout_u(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
                                                  int max_steps, int32_t* steps_out, int32_t* winner) {
   __shared__ __attribute__((aligned(16))) CitOpt buf[ROLLOUT_BUF ? ROLLOUT_BUF : 1];
+#ifdef ROLL_CLOCK
+  unsigned long long rc0 = wall_clock64();
+#endif
   uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     uint64_t* sc = seer + l * CIT_SEER_MAX;
     int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
@@ -306,6 +315,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     steps_out[l] += s;
     winner[l] = g.winner;
   });
+#ifdef ROLL_CLOCK
+  if (threadIdx.x == 0 && blockIdx.x < 65536) {
+    g_roll_clock[2 * blockIdx.x] = rc0;
+    g_roll_clock[2 * blockIdx.x + 1] = wall_clock64();
+  }
+#endif
 }
 
 // config-3 position harness: k = random.randint(lo, hi) random steps per lane.
@@ -366,6 +381,12 @@ int cit_roll_prof_read(unsigned long long* out) {
   unsigned long long z[160] = {};
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_roll_prof), z, sizeof(z));
   return (int)e;
+}
+#endif
+
+#ifdef ROLL_CLOCK
+int cit_roll_clock_read(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_roll_clock), sizeof(unsigned long long) * 2 * n);
 }
 #endif
 

@@ -320,20 +320,27 @@ template <class At>
 CIT_HD double np_sum(At at, int n, uint32_t& err) { return np_sum_rec<5>(at, 0, n, err); }
 
 // RandomState.choice(range(n), p=p) (legacy): ValueError -> err, returns -1.
+// CFR_ERR_DIAG builds (tools/diag_cfr_errors.py) also record which check
+// raised: 0x200 empty, 0x400 NaN / negative, 0x800 sum != 1.
+#ifdef CFR_ERR_DIAG
+#define CFR_DIAG(b) (b)
+#else
+#define CFR_DIAG(b) 0u
+#endif
 template <class P>
 CIT_HD int np_choice(CitMT& rng, P p, int n, uint32_t& err) {
-  if (n <= 0) { err |= CIT_ERR_VALUE; return -1; }
+  if (n <= 0) { err |= CIT_ERR_VALUE | CFR_DIAG(0x200u); return -1; }
   double s = p(0), c = 0.0;
   for (int i = 0; i < n; i++) {
     double v = p(i);
-    if (v != v || v < 0) { err |= CIT_ERR_VALUE; return -1; }
+    if (v != v || v < 0) { err |= CIT_ERR_VALUE | CFR_DIAG(0x400u); return -1; }
     if (i) {
       double y = v - c, t = s + y;
       c = (t - s) - y;
       s = t;
     }
   }
-  if (fabs(s - 1.0) > CFR_ATOL) { err |= CIT_ERR_VALUE; return -1; }
+  if (fabs(s - 1.0) > CFR_ATOL) { err |= CIT_ERR_VALUE | CFR_DIAG(0x800u); return -1; }
   double tot = 0.0;
   for (int i = 0; i < n; i++) tot = i ? tot + p(i) : p(0);
   double u = mt_random(rng);

@@ -41,9 +41,11 @@ def collect(rank, world, args, phase, min_targets, log):
         if args.save_tuples:
             tuples += selfplay.targets_to_tuples(t)
         pooled += f.shape[0]
-        errs = int((stats[:, 4] != 0).sum())
-        log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), %d lanes with errors, %.1fs"
-            % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, errs, time.time() - t0))
+        term = t["terminal"].to(stats.device)
+        errs = int(((stats[:, 4] != 0) & ~term).sum())
+        log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), %d lanes with errors, "
+            "%d already-terminal positions, %.1fs"
+            % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, errs, int(term.sum()), time.time() - t0))
         rnd += 1
     return torch.cat(feats), torch.cat(values), tuples
 
@@ -51,7 +53,9 @@ def collect(rank, world, args, phase, min_targets, log):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200000)
-    ap.add_argument("--games-per-gpu", type=int, default=64)
+    # 160 cfr_train(200000) pools (~1.3 GB each, engine.pool_caps) fill ~210 GB of
+    # the 288 GB HBM3E: one launch per round (simulate_games chunks if they do not fit)
+    ap.add_argument("--games-per-gpu", type=int, default=160)
     ap.add_argument("--node-cap", type=int, default=None)
     ap.add_argument("--pretrain-targets", type=int, default=20000)
     ap.add_argument("--train-targets", type=int, default=5000)

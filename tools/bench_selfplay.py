@@ -43,11 +43,11 @@ def main():
     ap.add_argument("--seed", type=int, default=30_000_000)
     a = ap.parse_args()
     rank, world, dev = selfplay.init_distributed()
-    # config 5: 1024 trees per GPU at 20000 iterations (one wave per SIMD), 64 at
-    # the reference's 200000 (engine.pool_caps sizes the pools; ~1 GB per tree)
+    # config 5: 1024 trees per GPU at 20000 iterations (one wave per SIMD), 160 at
+    # the reference's 200000 (engine.pool_caps sizes the pools; ~1.3 GB per tree)
     iters = a.iters or {3: 200, 4: 200, 5: 20000}[a.config]
     B = a.batch or {3: 1024, 4: 4096 // max(1, world) if world > 1 else 4096,
-                    5: 1024 if iters <= 20000 else 64}[a.config]
+                    5: 1024 if iters <= 20000 else 160}[a.config]
     net = None
     if a.config == 4:
         from citadels_self_play_amd import models

@@ -330,6 +330,34 @@ serial:
 }
 // substract_from_known_hand_confidences_and_clear_wizard (agent.py:100-109), all owners
 CIT_HD void kh_decay(CitGame& g) {
+#if CIT_WAVE
+  {   // lane e holds entry e; a kept entry's cards move left by one lane-parallel
+      // copy (all lanes load before any stores), its record by one compaction store
+    const int n = g.n_kh, l = cit_lane();
+    CitKH k = g.kh[l < n ? l : 0];
+    const int len = l < n ? k.len : 0, conf = kh_conf(k) - 1;
+    const bool keep = l < n && conf != 0;
+    int ro = 0, wo = 0;
+    for (int e = 0; e < n; e++) {
+      int le = cit_readlane(len, e);
+      if (cit_readlane(conf, e) != 0) {
+        if (wo != ro)
+          for (int i = l; i < le; i += 64) {
+            int v = g.kh_pool[ro + i];
+            g.kh_pool[wo + i] = (uint8_t)v;
+          }
+        wo += le;
+      }
+      ro += le;
+    }
+    const uint64_t km = cit_ballot(keep);
+    k.conf_flags = (uint8_t)(conf & 15);
+    if (keep) g.kh[__popcll(km & cit_below())] = k;
+    g.n_kh = (uint8_t)__popcll(km);
+    g.kh_fill = (uint8_t)wo;
+    return;
+  }
+#endif
   int w = 0, wo = 0, ro = 0;
   for (int e = 0; e < g.n_kh; e++) {
     CitKH k = g.kh[e];
@@ -434,6 +462,22 @@ CIT_HD void at5(CitGame& g, int pid, int tok) {
 // ================================================================= setup
 // refresh_used_roles (game.py:349-357)
 CIT_HD void refresh_used_roles(CitGame& g) {
+#if CIT_WAVE
+  {   // lane i: player i's role rank; its place in the stable sort by counting
+    const int l = cit_lane();
+    const int role = g.pl[l < CIT_NP ? l : 0].role;
+    if (cit_ballot(l < CIT_NP && role != ROLE_BEWITCHED && role >= 27)) g.err |= CIT_ERR_KEY;
+    const int v = role == ROLE_BEWITCHED ? -1 : role >= 27 ? 0 : role / 3;
+    int pos = 0;
+    for (int j = 0; j < CIT_NP; j++) {
+      int vj = cit_readlane(v, j);
+      pos += (vj < v || (vj == v && j < l)) ? 1 : 0;
+    }
+    if (l < CIT_NP) g.used_roles[pos] = (int8_t)v;
+    g.n_used_roles = CIT_NP;
+    return;
+  }
+#endif
   int8_t v[CIT_NP];
   for (int i = 0; i < CIT_NP; i++) v[i] = (int8_t)role_rank(g, g.pl[i].role);
   for (int i = 1; i < CIT_NP; i++) {     // insertion sort
@@ -480,11 +524,16 @@ CIT_HD void setup_next_player(CitGame& g, int current) {
 CIT_HD void cit_setup_round(CitGame& g, CitMT& rng) {
   for (int r = 0; r < 8; r++) g.rp[r] = 0;
   g.n_used_roles = 0;
-  uint8_t pool[8];
-  for (int r = 0; r < 8; r++) pool[r] = (uint8_t)r;
-  shuffle_arr(rng, pool, 8);
+  // the 8 ranks shuffled (random.shuffle) as nibbles of one register word
+  uint32_t pool = 0x76543210u;
+  for (int i = 7; i > 0; i--) {
+    int j = (int)mt_randbelow(rng, (uint32_t)(i + 1));
+    uint32_t ai = (pool >> (4 * i)) & 15u, aj = (pool >> (4 * j)) & 15u;
+    pool &= ~((15u << (4 * i)) | (15u << (4 * j)));
+    pool |= (aj << (4 * i)) | (ai << (4 * j));
+  }
   uint8_t m = 0;
-  for (int r = 0; r < 7; r++) m |= (uint8_t)(1u << pool[r]);   // pool[7] is the face-down role
+  for (int r = 0; r < 7; r++) m |= (uint8_t)(1u << ((pool >> (4 * r)) & 15u));   // pool[7] is the face-down role
   g.rtc = m;
   int c = -1;
 #if CIT_WAVE

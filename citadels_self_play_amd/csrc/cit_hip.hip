@@ -253,27 +253,32 @@ __global__ void k_random_choice(uint32_t* games, uint32_t* mt, uint32_t* idx, in
 // tools/prof_rollout.py).  [0..4] prepare / enumerate / randbelow / pick /
 // carry_out cycles, [5] steps, [16+s] enumerate+carry cycles in state s,
 // [32+s] steps in state s, [64+o] carry_out cycles of option name o, [112+o] their count.
+// s_memtime stamps (clock64): reading one waits for the wave's outstanding LDS
+// operations, so a phase is also charged the drain of the previous phase's
+// LDS stores.  (HW_REG_SHADER_CYCLES reads 0 on gfx950.)
+__device__ __forceinline__ unsigned long long prof_clk() { return clock64(); }
+__device__ __forceinline__ unsigned long long prof_d(unsigned long long a, unsigned long long b) { return b - a; }
 __device__ int prof_step(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* buf, int cap, unsigned long long* acc) {
   int st = g.gs_state;
-  unsigned long long t0 = wall_clock64(), t0c = clock64();
+  unsigned long long t0c = prof_clk();
   cit_prepare_options(g, rng, seer);
-  unsigned long long t1 = clock64();
+  unsigned long long t1 = prof_clk();
   BufSink s(buf, cap);
   cit_enum_options(g, s, seer);
-  unsigned long long t2 = clock64();
+  unsigned long long t2 = prof_clk();
   if (s.err) { g.err |= s.err; return 1; }
   int n = s.n;
   if (n == 0) { g.err |= CIT_ERR_EMPTY; return 1; }
   int k = (int)mt_randbelow(rng, (uint32_t)n);
-  unsigned long long t3 = clock64();
+  unsigned long long t3 = prof_clk();
   CitOpt o = k < cap ? buf[k] : cit_pick_option(g, k, seer);
-  unsigned long long t4 = clock64();
+  unsigned long long t4 = prof_clk();
   int w = cit_carry_out(g, o, rng);
-  unsigned long long t5 = clock64();
-  (void)t0;
-  acc[0] += t1 - t0c; acc[1] += t2 - t1; acc[2] += t3 - t2; acc[3] += t4 - t3; acc[4] += t5 - t4; acc[5] += 1;
-  if (st < 11) { acc[16 + st] += (t2 - t1) + (t5 - t4); acc[32 + st] += 1; }
-  if (o.name < 47) { acc[64 + o.name] += t5 - t4; acc[112 + o.name] += 1; }
+  unsigned long long t5 = prof_clk();
+  acc[0] += prof_d(t0c, t1); acc[1] += prof_d(t1, t2); acc[2] += prof_d(t2, t3); acc[3] += prof_d(t3, t4);
+  acc[4] += prof_d(t4, t5); acc[5] += 1;
+  if (st < 11) { acc[16 + st] += prof_d(t1, t2) + prof_d(t4, t5); acc[32 + st] += 1; }
+  if (o.name < 47) { acc[64 + o.name] += prof_d(t4, t5); acc[112 + o.name] += 1; }
   return (w >= 0 || g.err || g.terminal) ? 1 : 0;
 }
 #endif

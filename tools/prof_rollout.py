@@ -1,7 +1,7 @@
 """Per-phase cycle accounting of the config-2 rollout step on the GPU.
 
 Builds a profiling variant of the library (-DCIT_PROF_ROLLOUT) into
-build/libcitprof_roll.so beforehand (`python tools/prof_rollout.py build`, on
+build/rollprof/libcitprof_roll.so beforehand (`python tools/prof_rollout.py build`, on
 the CPU); on the GPU box run `python tools/prof_rollout.py [B]`.  Prints mean
 shader-clock cycles per step for prepare / enumerate / randbelow / pick /
 carry_out and enumerate+carry cycles per game state."""
@@ -12,7 +12,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "build", "libcitprof_roll.so")
+LIB = os.path.join(ROOT, "build", "rollprof", "libcitprof_roll.so")
 sys.path.insert(0, ROOT)
 
 
@@ -28,9 +28,9 @@ def build():
     sys.path.insert(0, ROOT)
     import __graft_entry__ as G
     objs = []
-    os.makedirs(os.path.join(ROOT, "build", "prof"), exist_ok=True)
+    os.makedirs(os.path.join(ROOT, "build", "rollprof"), exist_ok=True)
     for u in ["cit_hip.hip"]:
-        o = os.path.join(ROOT, "build", "prof", u.replace(".hip", ".o"))
+        o = os.path.join(ROOT, "build", "rollprof", u.replace(".hip", ".o"))
         subprocess.check_call([G.HIPCC] + G.HIP_FLAGS + ["-DCIT_PROF_ROLLOUT", "-c", os.path.join(G.CSRC, u), "-o", o])
         objs.append(o)
     subprocess.check_call([G.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + [os.path.join(ROOT, "build", "hip", u.replace(".hip", ".o")) for u in G.HIP_UNITS[1:]] + ["-o", LIB])

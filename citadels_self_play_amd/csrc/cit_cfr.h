@@ -327,9 +327,42 @@ CIT_HD double np_sum(At at, int n, uint32_t& err) { return np_sum_rec<5>(at, 0, 
 #else
 #define CFR_DIAG(b) 0u
 #endif
+#if CIT_WAVE
+__device__ __forceinline__ double cfr_readlane_f64(double v, int i) {
+  uint64_t b = __builtin_bit_cast(uint64_t, v);
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, i);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), i);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+#endif
 template <class P>
 CIT_HD int np_choice(CitMT& rng, P p, int n, uint32_t& err) {
   if (n <= 0) { err |= CIT_ERR_VALUE | CFR_DIAG(0x200u); return -1; }
+#if CIT_WAVE
+  if (n <= 64) {
+    // p(i) once, on lane i; the Kahan check and the cumulative sums run in
+    // index order as in numpy, and the n comparisons cum_i / cdf[-1] <= u
+    // (one division each) on the lanes.
+    const int l = (int)__lane_id();
+    const double v = l < n ? p(l) : 0.0;
+    if (__ballot(l < n && (v != v || v < 0))) { err |= CIT_ERR_VALUE | CFR_DIAG(0x400u); return -1; }
+    double s = cfr_readlane_f64(v, 0), c = 0.0, cum = s, mycum = s;
+    for (int i = 1; i < n; i++) {
+      double vi = cfr_readlane_f64(v, i);
+      double y = vi - c, t = s + y;
+      c = (t - s) - y;
+      s = t;
+      cum = cum + vi;
+      mycum = l == i ? cum : mycum;
+    }
+    if (fabs(s - 1.0) > CFR_ATOL) { err |= CIT_ERR_VALUE | CFR_DIAG(0x800u); return -1; }
+    const double tot = cum;
+    double u = mt_random(rng);
+    uint64_t m = __ballot(l < n && mycum / tot <= u);
+    int idx = m ? 64 - __clzll((long long)m) : 0;
+    return idx < n ? idx : n - 1;
+  }
+#endif
   double s = p(0), c = 0.0;
   for (int i = 0; i < n; i++) {
     double v = p(i);

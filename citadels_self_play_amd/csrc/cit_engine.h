@@ -2103,17 +2103,20 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
     uint64_t lm = cit_ballot(uu && ktarget == -1);
     g.n_deck = 0;
     g.deck_head = 0;
+    int lo = 0, kk = 0;
     if (lm) {
       int e = __ffsll((unsigned long long)lm) - 1;
-      int lo = cit_readlane(koff, e), ll = cit_readlane(klen, e);
-      int kk = ll < n ? ll : n;
-      nd = wave_append(deck_slot, 0, kk, [&g, lo](int i) { return (int)g.kh_pool[lo + i]; });
+      int ll = cit_readlane(klen, e);
+      lo = cit_readlane(koff, e);
+      kk = ll < n ? ll : n;
       n -= kk;
     }
     shuffle_arr(w, unk, nu);
     __syncthreads();
     int m = n < nu ? n : nu;
-    nd += wave_append(deck_slot, nd, m, [unk](int i) { return (int)unk[i]; });
+    // the known cards, then the shuffled unknowns: one compaction pass
+    nd = wave_append(deck_slot, 0, kk + m,
+                     [&g, unk, lo, kk](int i) { return i < kk ? (int)g.kh_pool[lo + i] : (int)unk[i - kk]; });
     head = m;
     g.n_deck = (uint8_t)nd;
   }
@@ -2160,20 +2163,21 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
   }
   for (int p = 0; p < CIT_NP; p++) {
     CitPlayer& Q = g.pl[p];
-    if (p != orig) {   // sample_cards_for_opponent (:264-280)
-      int n = Q.n_hand, nh = 0;
+    if (p != orig) {   // sample_cards_for_opponent (:264-280): known cards, then unknowns, one pass
+      int n = Q.n_hand, ho = 0, kk = 0;
       uint64_t hm = cit_ballot(uu && ktarget == p);
       if (hm) {
         int e = __ffsll((unsigned long long)hm) - 1;
-        int ho = cit_readlane(koff, e), hl = cit_readlane(klen, e);
-        int kk = hl < n ? hl : n;
-        nh = wave_append([&Q](int i) -> uint8_t& { return Q.hand[i & (CIT_HAND_CAP - 1)]; }, 0, kk,
-                         [&g, ho](int i) { return (int)g.kh_pool[ho + i]; });
+        int hl = cit_readlane(klen, e);
+        ho = cit_readlane(koff, e);
+        kk = hl < n ? hl : n;
         n -= kk;
       }
       int m = n < nu - head ? n : nu - head;
-      nh += wave_append([&Q](int i) -> uint8_t& { return Q.hand[i & (CIT_HAND_CAP - 1)]; }, nh, m,
-                        [unk, head](int i) { return (int)unk[head + i]; });
+      int nh = wave_append([&Q](int i) -> uint8_t& { return Q.hand[i & (CIT_HAND_CAP - 1)]; }, 0, kk + m,
+                           [&g, unk, ho, kk, head](int i) {
+                             return i < kk ? (int)g.kh_pool[ho + i] : (int)unk[head + i - kk];
+                           });
       head += m;
       Q.n_hand = (uint8_t)nh;
     }

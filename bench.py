@@ -29,6 +29,10 @@ Prints ONE JSON line on rank 0.  `value` = carry_out transitions of all ranks
   in the survey container; it cannot travel to the GPU box).
 * `e2e` adds the untimed init: games/s with k_init (seeding + deal) inside
   the timed region.
+* `roofline.latency`: one wave runs one game, so a launch lasts as long as
+  its longest game; steps_mean / steps_max is the share of the launch a
+  SIMD slot does useful work, and kernel time / steps_max the per-step
+  latency of that game (tools/rollout_clock.py).
 """
 import argparse
 import ctypes as C
@@ -277,6 +281,8 @@ def main():
 
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     trans_rank = sum(int(gb.steps.sum().item()) for gb in batches[W:])
+    # the launch lasts as long as its longest game (one wave per game, latency-bound)
+    steps_max = float(np.mean([int(gb.steps.max().item()) for gb in batches[W:]]))
     errs = sum(int((gb.errors() != 0).sum().item()) for gb in batches[W:])
     unfinished = sum(int((~gb.terminal()).sum().item()) for gb in batches[W:])
 
@@ -342,6 +348,10 @@ def main():
                          "alg_bytes_per_transition": 2 * L.GAME_BYTES,
                          "measured_gbs": (traffic / (avg_ms * 1e-3) / 1e9) if traffic else None,
                          "issue": issue_roofline(pmc.get("sq") if pmc else None, per_launch_trans, avg_ms),
+                         "latency": {"bound": "per-wave step latency x longest game",
+                                     "steps_mean": per_launch_trans / B, "steps_max_mean_per_launch": steps_max,
+                                     "us_per_step_longest_game": avg_ms * 1e3 / steps_max,
+                                     "mean_over_max": per_launch_trans / B / steps_max},
                          "pmc": pmc},
             "e2e": {"games_per_s": world * B * K / elapsed_e2e, "transitions_per_s": trans_all / elapsed_e2e,
                     "init_ms_per_batch": init_ms,

@@ -64,12 +64,40 @@ static_assert(sizeof(CfrEdge) == 48, "CfrEdge layout");
 static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
 #define CFR_ROLE_EDGE_SLOTS (CFR_ROLE_CHILDREN * 4)   // 10 edges + 10 wide records
 
+// Node pool of B trees, allocated in blocks from one arena as the trees grow
+// (a tree takes what it uses, not its worst case: a cfr_train(200000) tree
+// averages ~270k nodes against a ~650k-node maximum):
+//   per tree l (cfr_pool_bytes each): int32 node-block table [nblocks(node_cap)]
+//     | int32 edge-block table [eblocks(edge_cap)] | pad to 16 B
+//   arena (at B * cfr_pool_bytes): CfrArena header (64 B) | node records
+//     [n_cap blocks][CFR_NB] | node game rows [n_cap blocks][CFR_NB] (16-byte
+//     aligned, copied as 16-byte words) | edges [e_cap blocks][CFR_EB]
+// Node id n lives in block nbt[n >> CFR_NB_SHIFT] at slot n & (CFR_NB - 1);
+// edge index e likewise through ebt.  An edge run (a node's children) never
+// straddles an edge block.  Sizes are 64-bit.
+#define CFR_NB_SHIFT 12
+#define CFR_NB (1 << CFR_NB_SHIFT)            // nodes (records + rows) per block: 7 MB
+#define CFR_EB_SHIFT 14
+#define CFR_EB (1 << CFR_EB_SHIFT)            // edge slots per block: 768 KB
+#define CFR_TBL_MAX 1024                      // table entries a device tree keeps in LDS
+struct CfrArena {                             // 64 B, written by cit_cfr_arena_reset
+  uint32_t n_next, n_cap, e_next, e_cap;      // blocks handed out / capacity
+  uint32_t pad[12];
+};
+static_assert(sizeof(CfrArena) == 64, "CfrArena layout");
+
 struct CfrTree {
-  CfrNode* nodes;
-  CfrEdge* edges;
-  uint32_t* rows;                      // node_cap rows of CIT_GAME_BYTES
+  uint8_t* node_base;                  // arena node records
+  uint8_t* row_base;                   // arena node rows
+  uint8_t* edge_base;                  // arena edges
+  CfrArena* arena;
+  int32_t* nbt;                        // node-block table (LDS copy on the device)
+  int32_t* ebt;                        // edge-block table (LDS copy on the device)
+  int32_t* nbt_hbm;                    // the tree's tables in the pool
+  int32_t* ebt_hbm;
   int node_cap, edge_cap;
   int n_nodes, n_edges;
+  int n_eblk;                          // edge blocks held
   int orig;
   bool training;
   CitMT py;                            // the games' CPython stream
@@ -84,22 +112,30 @@ struct CfrTree {
   uint32_t carry_outs;
 };
 
-// Node pool of one tree: [node_cap CfrNode][edge_cap CfrEdge][pad to 16 B]
-// [node_cap rows]; B trees are B consecutive pools (every pool and row starts
-// 16-byte aligned, so rows move as 16-byte words).  Sizes are 64-bit: a
-// cfr_train(200000) tree needs ~0.5-1 GB.
-CIT_HD int64_t cfr_rows_offset(int node_cap, int edge_cap) {
-  int64_t o = (int64_t)node_cap * (int64_t)sizeof(CfrNode) + (int64_t)edge_cap * (int64_t)sizeof(CfrEdge);
-  return (o + 15) & ~(int64_t)15;
+CIT_HD int cfr_nblocks(int node_cap) { return (node_cap + CFR_NB - 1) >> CFR_NB_SHIFT; }
+CIT_HD int cfr_eblocks(int edge_cap) { return (edge_cap + CFR_EB - 1) >> CFR_EB_SHIFT; }
+CIT_HD int64_t cfr_pool_bytes(int node_cap, int edge_cap) {   // per tree: its two block tables
+  return ((int64_t)4 * (cfr_nblocks(node_cap) + cfr_eblocks(edge_cap)) + 15) & ~(int64_t)15;
 }
-CIT_HD int64_t cfr_pool_bytes(int node_cap, int edge_cap) {
-  return cfr_rows_offset(node_cap, edge_cap) + (int64_t)node_cap * CIT_GAME_BYTES;
+CIT_HD int64_t cfr_node_block_bytes() { return (int64_t)CFR_NB * (int64_t)(sizeof(CfrNode) + CIT_GAME_BYTES); }
+CIT_HD int64_t cfr_arena_bytes(int n_blocks, int e_blocks) {
+  return (int64_t)sizeof(CfrArena) + (int64_t)n_blocks * cfr_node_block_bytes() +
+         (int64_t)e_blocks * CFR_EB * (int64_t)sizeof(CfrEdge);
 }
-CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, long l, int node_cap, int edge_cap) {
-  uint8_t* base = pool + cfr_pool_bytes(node_cap, edge_cap) * (int64_t)l;
-  T.nodes = reinterpret_cast<CfrNode*>(base);
-  T.edges = reinterpret_cast<CfrEdge*>(base + (int64_t)node_cap * (int64_t)sizeof(CfrNode));
-  T.rows = reinterpret_cast<uint32_t*>(base + cfr_rows_offset(node_cap, edge_cap));
+// Binds tree l of a B-tree pool; the arena's capacities come from its header.
+CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, int B, long l, int node_cap, int edge_cap) {
+  int64_t per = cfr_pool_bytes(node_cap, edge_cap);
+  int32_t* tbl = reinterpret_cast<int32_t*>(pool + per * (int64_t)l);
+  T.nbt_hbm = tbl;
+  T.ebt_hbm = tbl + cfr_nblocks(node_cap);
+  T.nbt = T.nbt_hbm;
+  T.ebt = T.ebt_hbm;
+  uint8_t* a = pool + per * (int64_t)B;
+  T.arena = reinterpret_cast<CfrArena*>(a);
+  int64_t ncap = T.arena->n_cap;
+  T.node_base = a + sizeof(CfrArena);
+  T.row_base = T.node_base + ncap * CFR_NB * (int64_t)sizeof(CfrNode);
+  T.edge_base = T.row_base + ncap * CFR_NB * (int64_t)CIT_GAME_BYTES;
   T.node_cap = node_cap;
   T.edge_cap = edge_cap;
 }
@@ -171,6 +207,7 @@ CIT_HD CitOpt cfr_uopt(const CitOpt& o) { return o; }
 #if defined(__HIPCC__)
 struct CfrLds {
   uint32_t w[2][CIT_GAME_BYTES / 4];
+  int32_t nbt[CFR_TBL_MAX], ebt[CFR_TBL_MAX];     // the tree's block tables
   CitOpt lbuf[CFR_LBUF];
   double sbuf[CFR_OPT_CAP], cbuf[CFR_OPT_CAP];   // update_strategy: S, CS of node `cnode`
   uint32_t py[CIT_MT_N], np[CIT_MT_N];
@@ -196,13 +233,46 @@ CIT_HD CitGame& cfr_w(const CfrTree& T, int which) { return which ? *T.w1 : *T.w
 CIT_HD CitOpt* cfr_lbuf(const CfrTree& T) { return T.lbuf; }
 CIT_HD uint8_t* cfr_tmp(const CfrTree& T) { return T.tmp; }
 #endif
-CIT_HD CfrNode* cfr_nd(const CfrTree& T) { return cfr_glb(T.nodes); }
-CIT_HD CfrEdge* cfr_ed(const CfrTree& T) { return cfr_glb(T.edges); }
+// One block from an arena counter (lane 0's atomic on the device); -1 when
+// the arena is full.
+CIT_HD int cfr_take_block(uint32_t* next, uint32_t cap) {
+#if CIT_WAVE
+  uint32_t v = 0;
+  if (__lane_id() == 0) v = atomicAdd(next, 1u);
+  v = cfr_u(v);
+#else
+  uint32_t v = (*next)++;
+#endif
+  return v < cap ? (int)v : -1;
+}
+
+// The block tables: LDS (fixed addresses) in a device search, else the pool's.
+#if CIT_WAVE
+__device__ __forceinline__ int32_t* cfr_nbt(const CfrTree&) { return cfr_ls.nbt; }
+__device__ __forceinline__ int32_t* cfr_ebt(const CfrTree&) { return cfr_ls.ebt; }
+#else
+CIT_HD int32_t* cfr_nbt(const CfrTree& T) { return T.nbt; }
+CIT_HD int32_t* cfr_ebt(const CfrTree& T) { return T.ebt; }
+#endif
+
+// node n's record, edge e (a run of edges continues from it), node n's row
+CIT_HD int64_t cfr_node_slot(const CfrTree& T, int n) {
+  return (int64_t)cfr_nbt(T)[n >> CFR_NB_SHIFT] * CFR_NB + (n & (CFR_NB - 1));
+}
+CIT_HD CfrNode& cfr_node(const CfrTree& T, int n) {
+  return *reinterpret_cast<CfrNode*>(cfr_glb(T.node_base) + cfr_node_slot(T, n) * (int64_t)sizeof(CfrNode));
+}
+CIT_HD CfrEdge* cfr_edge(const CfrTree& T, int e) {
+  int64_t slot = (int64_t)cfr_ebt(T)[e >> CFR_EB_SHIFT] * CFR_EB + (e & (CFR_EB - 1));
+  return reinterpret_cast<CfrEdge*>(cfr_glb(T.edge_base) + slot * (int64_t)sizeof(CfrEdge));
+}
 // the [6]-wide regret / strategy columns of role-pick child a
 CIT_HD CfrWide* cfr_wide(const CfrTree& T, int first_edge) {
-  return reinterpret_cast<CfrWide*>(cfr_ed(T) + first_edge + CFR_ROLE_CHILDREN);
+  return reinterpret_cast<CfrWide*>(cfr_edge(T, first_edge) + CFR_ROLE_CHILDREN);
 }
-CIT_HD uint32_t* row_of(const CfrTree& T, int id) { return cfr_glb(T.rows) + (long)id * (CIT_GAME_BYTES / 4); }
+CIT_HD uint32_t* row_of(const CfrTree& T, int id) {
+  return reinterpret_cast<uint32_t*>(cfr_glb(T.row_base) + cfr_node_slot(T, id) * (int64_t)CIT_GAME_BYTES);
+}
 CIT_HD uint32_t* w_row(const CfrTree& T, int which) { return reinterpret_cast<uint32_t*>(&cfr_w(T, which)); }
 
 // One out-of-line copy of each engine entry point for the search: the
@@ -500,8 +570,14 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   }
   T.err |= e | w.err;
   if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
-  int id = T.n_nodes++;
-  CfrNode& N = cfr_nd(T)[id];
+  int id = T.n_nodes;
+  if ((id & (CFR_NB - 1)) == 0) {       // the first node of a new block
+    int b = cfr_take_block(&cfr_glb(T.arena)->n_next, cfr_glb(T.arena)->n_cap);
+    if (b < 0) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+    cfr_nbt(T)[id >> CFR_NB_SHIFT] = b;
+  }
+  T.n_nodes = id + 1;
+  CfrNode& N = cfr_node(T, id);
 #if CIT_WAVE
   {   // the header's 6 words and the 36 zero words of nv / wp / pred, one store per lane
     uint32_t hw[6];
@@ -533,10 +609,17 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   return id;
 }
 
+// A run of n edge slots (a node's children) inside one edge block.
 CIT_HD int alloc_edges(CfrTree& T, int n) {
-  if (T.n_edges + n > T.edge_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
   int f = T.n_edges;
-  T.n_edges += n;
+  if ((f & (CFR_EB - 1)) + n > CFR_EB) f = (f | (CFR_EB - 1)) + 1;
+  if (f + n > T.edge_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+  while (((f + n - 1) >> CFR_EB_SHIFT) >= T.n_eblk) {
+    int b = cfr_take_block(&cfr_glb(T.arena)->e_next, cfr_glb(T.arena)->e_cap);
+    if (b < 0) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+    cfr_ebt(T)[T.n_eblk++] = b;
+  }
+  T.n_edges = f + n;
   return f;
 }
 CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
@@ -550,16 +633,14 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(8);            // :102-131
   n = cfr_u(n);
-  CfrNode* ND = cfr_nd(T);
-  CfrEdge* ED = cfr_ed(T);
   int f = alloc_edges(T, CFR_ROLE_EDGE_SLOTS);
   if (f < 0) return;
   CfrWide* W = cfr_wide(T, f);
   for (int r = 0; r < CFR_ROLE_CHILDREN; r++)
     for (int k = 0; k < 6; k++) W[r].R[k] = W[r].S[k] = W[r].CS[k] = 0.0;
-  ND[n].first_edge = f;
-  ND[n].edge_cap = CFR_ROLE_CHILDREN;
-  int depth = ND[n].depth + 1;
+  cfr_node(T, n).first_edge = f;
+  cfr_node(T, n).edge_cap = CFR_ROLE_CHILDREN;
+  int depth = cfr_node(T, n).depth + 1;
   CitGame& h = cfr_w(T, 1);
   for (int r = 0; r < CFR_ROLE_CHILDREN && !T.err; r++) {
     copy_row(T, w_row(T, 1), row_of(T, n));
@@ -579,8 +660,8 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
     if (T.err) return;
     int c = cfr_u(cfr_node(T, 1, n, depth, 0));
     if (c < 0) return;
-    init_edge(ED[f + r], last, c);
-    ND[n].n_children = (int16_t)(r + 1);
+    init_edge((*cfr_edge(T, f + r)), last, c);
+    cfr_node(T, n).n_children = (int16_t)(r + 1);
   }
 }
 
@@ -588,8 +669,6 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(9);                   // :133-151
   n = cfr_u(n);
-  CfrNode* ND = cfr_nd(T);
-  CfrEdge* ED = cfr_ed(T);
   CitGame& g = cfr_w(T, 0);
   copy_row(T, w_row(T, 0), row_of(T, n));
   eng_prepare(T, 0);
@@ -602,12 +681,12 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
   int cnt = nl;
   int f = alloc_edges(T, cnt);
   if (f < 0) return;
-  CfrNode& N = ND[n];
+  CfrNode& N = cfr_node(T, n);
   N.first_edge = f;
   N.edge_cap = (int16_t)cnt;
   int par = N.parent;
-  bool sample = par < 0 || N.player != ND[par].player;
-  bool role_sample = par >= 0 && ND[par].gs_state != 0;
+  bool sample = par < 0 || N.player != cfr_node(T, par).player;
+  bool role_sample = par >= 0 && cfr_node(T, par).gs_state != 0;
   int depth = N.depth + 1;
   const CitOpt* ob = cfr_glb(T.optbuf);
   CitGame& h = cfr_w(T, 1);
@@ -621,8 +700,8 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
     if (T.err) return;
     int c = cfr_u(cfr_node(T, 1, n, depth, 0));
     if (c < 0) return;
-    init_edge(ED[f + i], o, c);
-    ND[n].n_children = (int16_t)(i + 1);
+    init_edge((*cfr_edge(T, f + i)), o, c);
+    cfr_node(T, n).n_children = (int16_t)(i + 1);
   }
 }
 
@@ -630,13 +709,11 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(10);              // :153-179
   n = cfr_u(n);
-  CfrNode* ND = cfr_nd(T);
-  CfrEdge* ED = cfr_ed(T);
-  CfrNode& N = ND[n];
+  CfrNode& N = cfr_node(T, n);
   copy_row(T, w_row(T, 1), row_of(T, n));
   CitGame& h = cfr_w(T, 1);
   int par = N.parent;
-  if (par < 0 || N.player != ND[par].player) eng_sample(T, 1, T.orig, par >= 0 && ND[par].gs_state != 0);
+  if (par < 0 || N.player != cfr_node(T, par).player) eng_sample(T, 1, T.orig, par >= 0 && cfr_node(T, par).gs_state != 0);
   eng_prepare(T, 1);
   CfrCnt lc = cfr_ucnt(eng_list_lds(T, 1));
   T.err |= lc.err | h.err;
@@ -649,7 +726,7 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
   T.err |= h.err;
   if (T.err) return;
   for (int j = 0; j < N.n_children; j++)
-    if (opt_eq(ED[N.first_edge + j].opt, key)) return;
+    if (opt_eq((*cfr_edge(T, N.first_edge + j)).opt, key)) return;
   if (N.first_edge < 0) {
     int f = alloc_edges(T, CFR_OPP_CHILDREN);
     if (f < 0) return;
@@ -658,12 +735,12 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
   }
   int c = cfr_u(cfr_node(T, 1, n, N.depth + 1, 0));
   if (c < 0) return;
-  init_edge(ED[ND[n].first_edge + ND[n].n_children], key, c);
-  ND[n].n_children++;
+  init_edge((*cfr_edge(T, cfr_node(T, n).first_edge + cfr_node(T, n).n_children)), key, c);
+  cfr_node(T, n).n_children++;
 }
 
 CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
-  CfrNode& N = cfr_nd(T)[n];
+  CfrNode& N = cfr_node(T, n);
   if (N.gs_state == 0 && N.n_children == 0) {
     N.flags |= NF_ROLE_PICK;
     cfr_expand_role_pick(T, n);
@@ -679,10 +756,10 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(11);               // :292-319
   n = cfr_u(n);
-  CfrNode& N = cfr_nd(T)[n];
+  CfrNode& N = cfr_node(T, n);
   int nch = N.n_children;
   if (nch == 0) return;
-  CfrEdge* E = cfr_ed(T) + N.first_edge;
+  CfrEdge* E = cfr_edge(T, N.first_edge);
 #if CIT_WAVE
   if (!(N.flags & NF_ROLE_PICK)) {
     // lane a (a + 64, ...) owns edge a; the numpy sums run in their serial
@@ -752,9 +829,9 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(12);
   n = cfr_u(n);
-  CfrNode& N = cfr_nd(T)[n];
+  CfrNode& N = cfr_node(T, n);
   int nch = N.n_children;
-  const CfrEdge* E = cfr_ed(T) + (N.first_edge < 0 ? 0 : N.first_edge);
+  const CfrEdge* E = cfr_edge(T, N.first_edge < 0 ? 0 : N.first_edge);
   if (!(N.flags & NF_ROLE_PICK)) {
 #if CIT_WAVE
     if (cfr_ls.cnode == n && cfr_ls.cnch == nch) {   // update_strategy(n) left CS in LDS
@@ -788,22 +865,21 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(13);                // :231-256
   n = cfr_u(n);
-  CfrNode* ND = cfr_nd(T);
-  CfrNode& N = ND[n];
-  CfrEdge* E = cfr_ed(T) + N.first_edge;
+  CfrNode& N = cfr_node(T, n);
+  CfrEdge* E = cfr_edge(T, N.first_edge);
   int nch = N.n_children;
   if (!(N.flags & NF_ROLE_PICK)) {
     int p = N.player;
-    double mx = ND[E[0].child].wp[p];
+    double mx = cfr_node(T, E[0].child).wp[p];
     for (int a = 1; a < nch; a++) {
-      double v = ND[E[a].child].wp[p];
+      double v = cfr_node(T, E[a].child).wp[p];
       if (v > mx) mx = v;
     }
-    for (int a = 0; a < nch; a++) E[a].R += mx - ND[E[a].child].wp[p];
+    for (int a = 0; a < nch; a++) E[a].R += mx - cfr_node(T, E[a].child).wp[p];
   } else {
     CfrWide* W = cfr_wide(T, N.first_edge);
     for (int a = 0; a < nch; a++) {
-      const double* wp = ND[E[a].child].wp;
+      const double* wp = cfr_node(T, E[a].child).wp;
       double mx = wp[0];
       for (int p = 1; p < 6; p++) mx = (mx != mx || wp[p] != wp[p]) ? NAN : (wp[p] > mx ? wp[p] : mx);
       for (int p = 0; p < 6; p++) W[a].R[p] += mx - wp[p];
@@ -818,9 +894,8 @@ CIT_NOINLINE void cfr_backprop(CfrTree& T_in, int n, double r0, double r1, doubl
   CIT_PROF_SCOPE(14);   // :276-290
   n = cfr_u(n);
   const double reward[6] = {r0, r1, r2, r3, r4, r5};
-  CfrNode* ND = cfr_nd(T);
   while (n >= 0) {
-    CfrNode& N = ND[n];
+    CfrNode& N = cfr_node(T, n);
     double s0 = 0.0;
     for (int k = 0; k < 6; k++) s0 += N.nv[k];
     if (T.training || s0 == 0.0 || !model)
@@ -842,21 +917,19 @@ CIT_HD void cfr_backprop_arr(CfrTree& T, int n, const double* rw, bool model) {
 // CFRNode).  Returns the root id.
 CIT_HD int cfr_train(CfrTree& T_in, int iters, bool root_skipped = false) {
   CfrTree& T = CFR_T(T_in);
-  CfrNode* ND = cfr_nd(T);
-  CfrEdge* ED = cfr_ed(T);
   int root = cfr_u(cfr_node(T, 0, -1, 0, root_skipped ? 1 : 0));
   if (root < 0 || T.err) return root;
-  if (ND[root].flags & NF_TERMINAL) return root;
+  if (cfr_node(T, root).flags & NF_TERMINAL) return root;
   cfr_expand(T, root);
   int n = root;
   for (int it = 0; it < iters && !T.err; it++) {
     cfr_update_strategy(T, n);
     int a = cfr_u(cfr_choose(T, n));
     if (T.err) break;
-    n = ED[ND[n].first_edge + a].child;
-    if (ND[n].flags & NF_TERMINAL) {
+    n = (*cfr_edge(T, cfr_node(T, n).first_edge + a)).child;
+    if (cfr_node(T, n).flags & NF_TERMINAL) {
       double rw[6] = {0, 0, 0, 0, 0, 0};
-      if (ND[n].winner >= 0) rw[ND[n].winner] = 1.0;
+      if (cfr_node(T, n).winner >= 0) rw[cfr_node(T, n).winner] = 1.0;
       cfr_backprop_arr(T, n, rw, false);
       cfr_update_strategy(T, n);
       n = root;
@@ -873,11 +946,11 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(15);
   root = cfr_u(root);
-  CfrNode& N = cfr_nd(T)[root];
+  CfrNode& N = cfr_node(T, root);
   if (!(N.flags & NF_ROLE_PICK)) {
     int a = cfr_u(cfr_choose(T, root));
     if (T.err || a < 0) return mk(O_NUM_NAMES, 0);
-    return cfr_ed(T)[N.first_edge + a].opt;
+    return (*cfr_edge(T, N.first_edge + a)).opt;
   }
   CitGame& g = cfr_w(T, 0);
   copy_row(T, w_row(T, 0), row_of(T, root));
@@ -908,6 +981,7 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
 CIT_HD void cfr_state_load(CfrTree& T, const CfrState& S) {
   T.n_nodes = S.n_nodes;
   T.n_edges = S.n_edges;
+  T.n_eblk = (S.n_edges + CFR_EB - 1) >> CFR_EB_SHIFT;
   T.err = (uint32_t)S.err;
   T.carry_outs = (uint32_t)S.carry_outs;
   T.orig = S.orig;
@@ -923,7 +997,7 @@ CIT_NOINLINE void cfr_write_feat(CfrTree& T_in, int n, float* feat) {
   CfrTree& T = CFR_T(T_in);
   n = cfr_u(n);
   const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
-  int pid = (cfr_nd(T)[n].flags & NF_ROLE_PICK) ? 5 : -1;
+  int pid = (cfr_node(T, n).flags & NF_ROLE_PICK) ? 5 : -1;
   CFR_SYNC();
   cit_encode_game(g, cfr_glb(feat), pid);   // the whole team (identical stores): the engine's scans are wave-wide
   CFR_SYNC();
@@ -939,15 +1013,13 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
   iters = cfr_u(iters);
   max_depth = cfr_u(max_depth);
   const float* probs = cfr_glb(probs_in);
-  CfrNode* ND = cfr_nd(T);
-  CfrEdge* ED = cfr_ed(T);
   if (S.phase == CP_DONE) return 0;
   if (S.phase == CP_INIT) {
     S.orig = T.orig;
     int root = cfr_u(cfr_node(T, 0, -1, 0, root_skipped ? 1 : 0));
     S.root = root;
     S.it = 0;
-    if (root < 0 || T.err || (ND[root].flags & NF_TERMINAL)) {
+    if (root < 0 || T.err || (cfr_node(T, root).flags & NF_TERMINAL)) {
       if (root >= 0 && !T.err) T.err |= CIT_ERR_VALUE;   // action_choice on a childless root raises
       S.phase = CP_DONE;
       chosen = mk(O_NUM_NAMES, 0);
@@ -958,7 +1030,7 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
     S.phase = CP_RUN;
   } else if (S.phase == CP_WAIT) {
     int n = S.pending;
-    CfrNode& N = ND[n];
+    CfrNode& N = cfr_node(T, n);
     for (int k = 0; k < 6; k++) N.pred[k] = (double)(5.0f * probs[k]);   // model_reward_weights * wp (float32)
     N.flags |= NF_PRED;
     cfr_backprop_arr(T, n, N.pred, true);
@@ -971,18 +1043,18 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
     cfr_update_strategy(T, S.cur);
     int a = cfr_u(cfr_choose(T, S.cur));
     if (T.err) break;
-    int n = ED[ND[S.cur].first_edge + a].child;
-    CfrNode& N = ND[n];
+    int n = (*cfr_edge(T, cfr_node(T, S.cur).first_edge + a)).child;
+    CfrNode& N = cfr_node(T, n);
     if (N.depth > max_depth && !(N.flags & NF_TERMINAL)) {
       cfr_expand(T, n);
       if (T.err) break;
-      if (!(ND[n].flags & NF_PRED)) {
+      if (!(cfr_node(T, n).flags & NF_PRED)) {
         cfr_write_feat(T, n, feat);
         S.pending = n;
         S.phase = CP_WAIT;
         return 1;
       }
-      cfr_backprop_arr(T, n, ND[n].pred, true);
+      cfr_backprop_arr(T, n, cfr_node(T, n).pred, true);
       cfr_update_strategy(T, n);
       S.cur = S.root;
     } else if (N.flags & NF_TERMINAL) {
@@ -1011,7 +1083,7 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
 #define CFR_TARGET_THRESHOLD 15.0
 
 CIT_HD bool cfr_is_target(const CfrTree& T, int n) {
-  const CfrNode& N = T.nodes[n];
+  const CfrNode& N = cfr_node(T, n);
   if (N.n_children <= 0) return false;
   double s = 0.0;
   for (int k = 0; k < 6; k++) s += N.nv[k];     // integer-valued: order-free
@@ -1021,23 +1093,23 @@ CIT_HD bool cfr_is_target(const CfrTree& T, int n) {
 // Pre-order successor within the subtree of `top` through parent links (-1
 // after its last node).
 CIT_HD int cfr_preorder_next(const CfrTree& T, int n, int top) {
-  const CfrNode& N = T.nodes[n];
-  if (N.n_children > 0) return T.edges[N.first_edge].child;
+  const CfrNode& N = cfr_node(T, n);
+  if (N.n_children > 0) return (*cfr_edge(T, N.first_edge)).child;
   for (;;) {
-    int p = T.nodes[n].parent;
+    int p = cfr_node(T, n).parent;
     if (n == top || p < 0) return -1;
-    const CfrNode& P = T.nodes[p];
+    const CfrNode& P = cfr_node(T, p);
     int j = 0;
-    while (j < P.n_children && T.edges[P.first_edge + j].child != n) j++;
-    if (j + 1 < P.n_children) return T.edges[P.first_edge + j + 1].child;
+    while (j < P.n_children && (*cfr_edge(T, P.first_edge + j)).child != n) j++;
+    if (j + 1 < P.n_children) return (*cfr_edge(T, P.first_edge + j + 1)).child;
     n = p;
   }
 }
 
 // The tree of lane l in a node pool (nodes | edges | rows per tree), read-only use.
-CIT_HD CfrTree cfr_tree_view(uint8_t* pool, long l, int node_cap, int edge_cap) {
+CIT_HD CfrTree cfr_tree_view(uint8_t* pool, int B, long l, int node_cap, int edge_cap) {
   CfrTree T;
-  cfr_tree_bind(T, pool, l, node_cap, edge_cap);
+  cfr_tree_bind(T, pool, B, l, node_cap, edge_cap);
   return T;
 }
 
@@ -1047,7 +1119,7 @@ CIT_HD CfrTree cfr_tree_view(uint8_t* pool, long l, int node_cap, int edge_cap) 
 enum { CFR_TGT_TREE = 0, CFR_TGT_ROOT = 1 };
 
 CIT_HD bool cfr_target_sel(const CfrTree& T, int n, int mode) {
-  return mode == CFR_TGT_ROOT ? T.nodes[n].n_children > 0 : cfr_is_target(T, n);
+  return mode == CFR_TGT_ROOT ? cfr_node(T, n).n_children > 0 : cfr_is_target(T, n);
 }
 CIT_HD int cfr_target_next(const CfrTree& T, int n, int top, int mode) {
   return mode == CFR_TGT_ROOT ? -1 : cfr_preorder_next(T, n, top);
@@ -1060,7 +1132,7 @@ CIT_HD void cfr_count_targets(const CfrTree& T, int root, int mode, int32_t& n_t
   for (int n = root; n >= 0; n = cfr_target_next(T, n, root, mode))
     if (cfr_target_sel(T, n, mode)) {
       n_targets++;
-      n_children += T.nodes[n].n_children;
+      n_children += cfr_node(T, n).n_children;
     }
 }
 
@@ -1075,9 +1147,9 @@ CIT_HD void cfr_emit_targets(const CfrTree& T, CitMT& py, int root, int mode, in
   int32_t t = t0, c = c0;
   for (int n = root; n >= 0; n = cfr_target_next(T, n, root, mode)) {
     if (!cfr_target_sel(T, n, mode)) continue;
-    const CfrNode& N = T.nodes[n];
+    const CfrNode& N = cfr_node(T, n);
     const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
-    const CfrEdge* E = T.edges + N.first_edge;
+    const CfrEdge* E = cfr_edge(T, N.first_edge);
     int pid = -1, row = 0;
     if (N.flags & NF_ROLE_PICK) {
       pid = (int)mt_randbelow(py, 6u);

@@ -37,13 +37,17 @@ __device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, 
   for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) mt[(long)i * B + l] = src[i];
 }
 
-// The tree's LDS block (cit_cfr.h, cfr_ls): pool binding, streams, working rows.
+// The tree's LDS block (cit_cfr.h, cfr_ls): pool binding (block tables in LDS),
+// streams, working rows.
 __device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx,
                                            uint64_t* seer, int B, long l, uint8_t* pool, int node_cap, int edge_cap,
                                            CitOpt* optbuf) {
   CfrTree& T = cfr_ls.T;
   cfr_ls.cnode = -1;
-  cfr_tree_bind(T, pool, l, node_cap, edge_cap);
+  cfr_tree_bind(T, pool, B, l, node_cap, edge_cap);
+  T.nbt = cfr_ls.nbt;
+  T.ebt = cfr_ls.ebt;
+  T.n_eblk = 0;
   T.training = false;
   T.py = mt_stage_in(cfr_ls.py, mt, idx, B, l);
   T.np = mt_stage_in(cfr_ls.np, npmt, npidx, B, l);
@@ -53,6 +57,20 @@ __device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t
   T.w1 = reinterpret_cast<CitGame*>(cfr_ls.w[1]);
   T.tmp = cfr_ls.tmp;
   T.lbuf = cfr_ls.lbuf;
+}
+
+// The block tables of a tree between LDS and its pool (n node / e edge blocks).
+__device__ __forceinline__ void tables_load(const CfrTree& T, int n_nodes, int n_edges) {
+  int nb = (n_nodes + CFR_NB - 1) >> CFR_NB_SHIFT, eb = (n_edges + CFR_EB - 1) >> CFR_EB_SHIFT;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) cfr_ls.nbt[i] = T.nbt_hbm[i];
+  for (int i = threadIdx.x; i < eb; i += blockDim.x) cfr_ls.ebt[i] = T.ebt_hbm[i];
+  __syncthreads();
+}
+__device__ __forceinline__ void tables_store(const CfrTree& T) {
+  __syncthreads();
+  int nb = (T.n_nodes + CFR_NB - 1) >> CFR_NB_SHIFT;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) T.nbt_hbm[i] = cfr_ls.nbt[i];
+  for (int i = threadIdx.x; i < T.n_eblk; i += blockDim.x) T.ebt_hbm[i] = cfr_ls.ebt[i];
 }
 
 // One MCCFR decision per workgroup: a 64-lane team runs the search on its
@@ -79,6 +97,7 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   CitOpt c = mk(O_NUM_NAMES, 0);
   if (root >= 0 && !T.err) c = cfr_uopt(cfr_live_choice(T, root));
   if (root >= 0) copy_row(T, games + l * ROW_W, row_of(T, root));
+  tables_store(T);
   mt_stage_out(cfr_ls.py, mt, B, l);
   mt_stage_out(cfr_ls.np, npmt, B, l);
   if (threadIdx.x == 0) {
@@ -122,6 +141,7 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
     T.orig = orig ? orig[l] : cfr_w(T, 0).gs_pid;
   } else {
     cfr_state_load(T, S);
+    tables_load(T, T.n_nodes, T.n_edges);
   }
   CitOpt c;
   int r = cfr_pred_run(T, S, iters, max_depth, probs + 6 * l, feat + (long)CIT_FEAT * l, c,
@@ -129,6 +149,7 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   r = cfr_u(r);
   cfr_state_save(T, S);
   if (!r && S.root >= 0) copy_row(T, games + l * ROW_W, row_of(T, S.root));
+  tables_store(T);
   mt_stage_out(cfr_ls.py, mt, B, l);
   mt_stage_out(cfr_ls.np, npmt, B, l);
   if (threadIdx.x == 0) {
@@ -138,6 +159,15 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
     npidx[l] = T.np.pos;
     if (r) atomicAdd(waiting, 1);
   }
+}
+
+// A pool before its trees start: every block-table entry -1, the arena
+// header with no blocks handed out and the given capacities.
+__global__ void k_arena_reset(int32_t* tables, long n_words, CfrArena* a, uint32_t n_cap, uint32_t e_cap) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_words) tables[i] = -1;
+  if (blockIdx.x == 0 && threadIdx.x < sizeof(CfrArena) / 4)
+    reinterpret_cast<uint32_t*>(a)[threadIdx.x] = threadIdx.x == 1 ? n_cap : threadIdx.x == 3 ? e_cap : 0u;
 }
 
 }  // namespace
@@ -151,16 +181,37 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
 extern "C" {
 
 int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap) {
-  if (node_cap <= 0 || edge_cap <= 0) return -1;
+  if (node_cap <= 0 || edge_cap <= 0 || cfr_nblocks(node_cap) > CFR_TBL_MAX || cfr_eblocks(edge_cap) > CFR_TBL_MAX)
+    return -1;
   return cfr_pool_bytes(node_cap, edge_cap);
+}
+int64_t cit_cfr_arena_bytes(int node_blocks, int edge_blocks) {
+  if (node_blocks < 0 || edge_blocks < 0) return -1;
+  return cfr_arena_bytes(node_blocks, edge_blocks);
+}
+int cit_cfr_block_sizes(int32_t* out) {
+  if (!out) return -1;
+  out[0] = CFR_NB;
+  out[1] = CFR_EB;
+  out[2] = CFR_TBL_MAX;
+  return 0;
+}
+int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                        hipStream_t stream) {
+  if (!pool || B <= 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || node_blocks < 0 || edge_blocks < 0) return -1;
+  long n_words = (long)(cfr_pool_bytes(node_cap, edge_cap) / 4) * B;
+  uint8_t* a = (uint8_t*)pool + n_words * 4;
+  hipLaunchKernelGGL(k_arena_reset, dim3((unsigned)((n_words + 255) / 256)), dim3(256), 0, stream, (int32_t*)pool,
+                     n_words, reinterpret_cast<CfrArena*>(a), (uint32_t)node_blocks, (uint32_t)edge_blocks);
+  CHECK_LAUNCH();
 }
 int cit_cfr_opt_cap(void) { return CFR_OPT_CAP; }
 
 int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
                    int B, int iters, int flags, const int32_t* orig_player, void* pool, int node_cap, int edge_cap,
                    CitOption* optbuf, CitOption* chosen, int32_t* stats, hipStream_t stream) {
-  if (B <= 0 || iters < 0 || node_cap <= 0 || edge_cap <= 0 || !games || !mt || !mt_idx || !np_mt || !np_idx ||
-      !seer || !pool || !optbuf || !chosen || !stats)
+  if (B <= 0 || iters < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt || !mt_idx || !np_mt ||
+      !np_idx || !seer || !pool || !optbuf || !chosen || !stats)
     return -1;
   hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
                      B, iters, flags, orig_player, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats);
@@ -173,8 +224,8 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
                       int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,
                       int node_cap, int edge_cap, CitOption* optbuf, void* state, const float* probs, float* feat,
                       CitOption* chosen, int32_t* waiting, hipStream_t stream) {
-  if (B <= 0 || iters < 0 || node_cap <= 0 || edge_cap <= 0 || !games || !mt || !mt_idx || !np_mt || !np_idx ||
-      !seer || !pool || !optbuf || !state || !probs || !feat || !chosen || !waiting)
+  if (B <= 0 || iters < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt || !mt_idx || !np_mt ||
+      !np_idx || !seer || !pool || !optbuf || !state || !probs || !feat || !chosen || !waiting)
     return -1;
   hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
                      seer, B, iters, flags, orig_player, max_depth, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,

@@ -146,6 +146,15 @@ void cith_advance_random(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer
 }
 
 int64_t cith_cfr_pool_bytes(int node_cap, int edge_cap) { return cfr_pool_bytes(node_cap, edge_cap); }
+int64_t cith_cfr_arena_bytes(int node_blocks, int edge_blocks) { return cfr_arena_bytes(node_blocks, edge_blocks); }
+void cith_cfr_arena_reset(uint8_t* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks) {
+  int64_t tb = cfr_pool_bytes(node_cap, edge_cap) * (int64_t)B;
+  memset(pool, 0xff, (size_t)tb);
+  CfrArena* a = reinterpret_cast<CfrArena*>(pool + tb);
+  memset(a, 0, sizeof(CfrArena));
+  a->n_cap = (uint32_t)node_blocks;
+  a->e_cap = (uint32_t)edge_blocks;
+}
 
 void cith_count_options(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int* n_opts) {
   for (int l = 0; l < B; l++) {
@@ -180,11 +189,13 @@ int cith_cfr_sizes(int* out) {
   out[0] = (int)sizeof(CfrNode);
   out[1] = (int)sizeof(CfrEdge);
   out[2] = CFR_OPT_CAP;
-  return 3;
+  out[3] = CFR_NB;
+  out[4] = CFR_EB;
+  return 5;
 }
 
-// run_mccfr(game, max_iterations=iters) without a model for every lane;
-// pool = per lane [node_cap CfrNode][edge_cap CfrEdge][node_cap rows].
+// run_mccfr(game, max_iterations=iters) without a model for every lane; pool
+// = B per-tree block tables + the arena (cit_cfr.h), header reset by the caller.
 // stats[l] = {root, n_nodes, n_edges, carry_outs, err}
 void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx, uint64_t* seer, int B,
                      int iters, int flags, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen, int* stats) {
@@ -194,7 +205,8 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
   CitOpt lbuf[CFR_LBUF];
   for (int l = 0; l < B; l++) {
     CfrTree T;
-    cfr_tree_bind(T, pool, l, node_cap, edge_cap);
+    cfr_tree_bind(T, pool, B, l, node_cap, edge_cap);
+    T.n_eblk = 0;
     T.n_nodes = T.n_edges = 0;
     T.orig = g[l].gs_pid;
     T.training = false;
@@ -247,7 +259,8 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
     CfrState& S = st[l];
     if (S.phase == CP_DONE) continue;
     CfrTree T;
-    cfr_tree_bind(T, pool, l, node_cap, edge_cap);
+    cfr_tree_bind(T, pool, B, l, node_cap, edge_cap);
+    T.n_eblk = 0;
     T.training = false;
     T.py = lane_rng(mt, idx, B, l);
     T.np = lane_rng(npmt, npidx, B, l);
@@ -312,7 +325,7 @@ void cith_close_position(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer
 
 void cith_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, const int* roots, int mode, int* counts) {
   for (int l = 0; l < B; l++) {
-    CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+    CfrTree T = cfr_tree_view(pool, B, l, node_cap, edge_cap);
     cfr_count_targets(T, roots[l], mode, counts[2 * l], counts[2 * l + 1]);
   }
 }
@@ -320,7 +333,7 @@ void cith_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, con
 void cith_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, const int* roots, int mode, uint32_t* mt,
                       uint32_t* idx, const int* offsets, int* meta, float* feat, double* value, double* dist, float* opt_feat) {
   for (int l = 0; l < B; l++) {
-    CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+    CfrTree T = cfr_tree_view(pool, B, l, node_cap, edge_cap);
     CitMT r = lane_rng(mt, idx, B, l);
     cfr_emit_targets(T, r, roots[l], mode, l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
     SAVE(r);

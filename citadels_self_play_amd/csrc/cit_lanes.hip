@@ -72,7 +72,7 @@ __global__ void k_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_
                                    int32_t* counts) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= B) return;
-  CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+  CfrTree T = cfr_tree_view(pool, B, l, node_cap, edge_cap);
   cfr_count_targets(T, roots[l], mode, counts[2 * l], counts[2 * l + 1]);
 }
 
@@ -82,7 +82,7 @@ __global__ void k_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, 
                               double* dist, float* opt_feat) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= B) return;
-  CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+  CfrTree T = cfr_tree_view(pool, B, l, node_cap, edge_cap);
   CitMT r = lane_mt(mt, idx, B, l);
   cfr_emit_targets(T, r, roots[l], mode, (int)l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
   idx[l] = r.pos;
@@ -95,12 +95,12 @@ __global__ void k_cfr_choose(uint8_t* pool, int B, int node_cap, int edge_cap, c
                              uint32_t* npidx, int32_t* edge_out, int32_t* err_out) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= B) return;
-  CfrTree T = cfr_tree_view(pool, l, node_cap, edge_cap);
+  CfrTree T = cfr_tree_view(pool, B, l, node_cap, edge_cap);
   T.np = lane_mt(npmt, npidx, B, l);
   T.err = 0;
   int n = node[l];
   int a = -1;
-  if (n < 0 || n >= node_cap || T.nodes[n].n_children <= 0) T.err |= CIT_ERR_VALUE;   // choice over []
+  if (n < 0 || n >= node_cap || cfr_node(T, n).n_children <= 0) T.err |= CIT_ERR_VALUE;   // choice over []
   else a = cfr_choose(T, n);
   edge_out[l] = T.err ? -1 : a;
   err_out[l] = (int32_t)T.err;

@@ -10,6 +10,8 @@ driven by the HIP kernels of libcitadels_hip.so.
 PyTorch supplies device memory and the stream; the compute is the native
 library.  Every call is asynchronous on torch's current stream.
 """
+import math
+
 import numpy as np
 import torch
 
@@ -49,6 +51,20 @@ def pool_caps(iters):
     pool is searched again with a 4x pool (GameBatch._retry_overflow)."""
     node_cap = max(1024, int(3.5 * iters) + 512)
     return node_cap, 4 * node_cap + 4096
+
+
+def arena_blocks(B, node_cap, edge_cap, frac=None):
+    """Arena blocks (node, edge) for B trees: `frac` (a number, or a (node, edge)
+    pair) of their worst case, at least one tree's worst case (None: all of it)."""
+    nbt, ebt = L.cfr_nblocks(node_cap), L.cfr_eblocks(edge_cap)
+    fn, fe = (1.0, 1.0) if frac is None else (frac if isinstance(frac, tuple) else (frac, frac))
+    return (min(B * nbt, max(nbt, math.ceil(fn * B * nbt))), min(B * ebt, max(ebt, math.ceil(fe * B * ebt))))
+
+
+def pool_bytes(B, node_cap, edge_cap, frac=None):
+    """Device bytes of a B-tree node pool: block tables + arena (cit_cfr.h)."""
+    nb, eb = arena_blocks(B, node_cap, edge_cap, frac)
+    return B * L.cfr_pool_bytes(node_cap, edge_cap) + L.cfr_arena_bytes(nb, eb)
 
 
 def _ptr(t):
@@ -164,20 +180,25 @@ class GameBatch:
 
     def _retry_overflow(self, snap, stats, chosen, run, max_retries, orig=None):
         """Lanes whose search overflowed its node / edge pool (stats err bit
-        CIT_ERR_OVERFLOW) are searched again from their pre-search state with a
-        4x larger pool; results and streams are scattered back, and the
+        CIT_ERR_OVERFLOW) are searched again from their pre-search state in a
+        batch of their own, with 4x the tree capacity (the same capacity when
+        it was the shared arena that ran out); results and streams are scattered back, and the
         sub-batch is kept so cfr_targets can read those lanes' trees."""
         self._retry = None
         over = ((stats[:, 4].to(self.device) & ERR_OVERFLOW) != 0).nonzero().flatten()
         if max_retries <= 0 or over.numel() == 0:
             return chosen, stats
+        (n_used, e_used), (n_cap, e_cap) = self.arena_used()
+        grow = 1 if (n_used > n_cap or e_used > e_cap) else 4    # the shared arena ran out: same tree caps
         g, mt, idx, seer, npm, npi, steps = snap
         sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),
                                      seer[over].contiguous(), npm[:, over].contiguous(), npi[over].contiguous())
         sub.steps = steps[over].contiguous()
         sub_orig = None if orig is None else \
             np.broadcast_to(np.asarray(orig, np.int32), (self.B,))[over.cpu().numpy()].copy()
-        c2, s2 = run(sub, 4 * self.node_cap, 4 * self.edge_cap, max_retries - 1, sub_orig)
+        nc = min(grow * self.node_cap, L.CFR_TBL_MAX * L.CFR_NB)
+        ec = min(grow * self.edge_cap, L.CFR_TBL_MAX * L.CFR_EB)
+        c2, s2 = run(sub, nc, ec, max_retries - 1, sub_orig)
         self.scatter(sub, over)
         chosen = chosen.clone()
         stats = stats.clone()
@@ -315,19 +336,45 @@ class GameBatch:
                                             _ptr(out["opt_feat"]), _stream()), "cit_cfr_targets")
         return out
 
+    arena_frac = None       # arena blocks as a fraction of the trees' worst case (arena_blocks)
+
     def _pool(self, node_cap, edge_cap):
+        """Node pool for B trees of (node_cap, edge_cap): block tables + an arena
+        of arena_blocks(..., self.arena_frac) blocks, reset (empty) for a new
+        search.  An arena that would not fit in device memory is cut to what
+        does; a tree that finds it exhausted overflows and is searched again
+        (_retry_overflow)."""
         edge_cap = edge_cap or 5 * node_cap
         per = self.lib.cit_cfr_pool_bytes(node_cap, edge_cap)
         if per <= 0 or node_cap >= 2 ** 31 or edge_cap >= 2 ** 31:
             raise ValueError("bad node pool capacity (%d nodes, %d edges)" % (node_cap, edge_cap))
-        need = per * self.B
-        if getattr(self, "pool", None) is not None and self.pool.numel() < need:
+        nb, eb = arena_blocks(self.B, node_cap, edge_cap, self.arena_frac)
+        need = per * self.B + self.lib.cit_cfr_arena_bytes(nb, eb)
+        have = self.pool.numel() if getattr(self, "pool", None) is not None else 0
+        if need > have and self.device.type == "cuda":
+            avail = int(0.9 * (torch.cuda.mem_get_info(self.device)[0] + have))
+            if need > avail:
+                nbt, ebt = L.cfr_nblocks(node_cap), L.cfr_eblocks(edge_cap)
+                scale = max(0.0, (avail - per * self.B) / float(need - per * self.B))
+                nb, eb = max(nbt, int(nb * scale)), max(ebt, int(eb * scale))
+                need = per * self.B + self.lib.cit_cfr_arena_bytes(nb, eb)
+        if have and have < need:
             self.pool = None                        # free the old pool before allocating the new one
             torch.cuda.empty_cache()
-        if getattr(self, "pool", None) is None or self.pool.numel() < need:
+        if getattr(self, "pool", None) is None:
             self.pool = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if getattr(self, "optbuf", None) is None or self.optbuf.shape[0] != self.B:
             self.optbuf = torch.empty((self.B, self.lib.cit_cfr_opt_cap(), 16), dtype=torch.uint8, device=self.device)
-        self.node_cap, self.edge_cap = node_cap, edge_cap
+        self.node_cap, self.edge_cap, self.arena = node_cap, edge_cap, (nb, eb)
+        _lib.check(self.lib.cit_cfr_arena_reset(_ptr(self.pool), self.B, node_cap, edge_cap, nb, eb, _stream()),
+                   "cit_cfr_arena_reset")
+
+    def arena_used(self):
+        """(node blocks, edge blocks) handed out by the last search's arena and its
+        capacity (node, edge); a count above capacity means it ran out."""
+        off = self.B * self.lib.cit_cfr_pool_bytes(self.node_cap, self.edge_cap)
+        h = self.pool[off:off + 16].cpu().numpy().view("<u4")
+        return (int(h[0]), int(h[2])), (int(h[1]), int(h[3]))
 
     def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000, max_retries=3,
                  flags=0, orig=None):
@@ -386,14 +433,9 @@ class GameBatch:
             over = retry[0].cpu().tolist()
             if lane in over:
                 return retry[1].tree(over.index(lane))
-        per = self.lib.cit_cfr_pool_bytes(self.node_cap, self.edge_cap)
-        base = self.pool[lane * per:(lane + 1) * per].cpu().numpy()
-        nb, eb = self.node_cap * NODE_DT.itemsize, self.edge_cap * EDGE_DT.itemsize
-        nodes = base[:nb].view(NODE_DT)
-        edges = base[nb:nb + eb].view(EDGE_DT)
-        ro = (nb + eb + 15) // 16 * 16                # rows start 16-byte aligned (cit_cfr.h cfr_rows_offset)
-        rows = base[ro:ro + self.node_cap * L.GAME_BYTES].reshape(self.node_cap, L.GAME_BYTES)
-        return nodes, edges, rows
+        nodes, edges, rows = L.cfr_tree_bytes(lambda o, n: self.pool[o:o + n].cpu().numpy(), self.B, lane,
+                                              self.node_cap, self.edge_cap)
+        return nodes.view(NODE_DT), edges.view(EDGE_DT), rows
 
     # --- single-game pieces of the search, exposed for the object API -------------
     def count_options(self):

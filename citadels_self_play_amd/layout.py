@@ -77,3 +77,65 @@ def game_from_bytes(b):
 
 def opt_from_bytes(b):
     return CitOpt.from_buffer_copy(bytes(b)[:16])
+
+
+# ---- MCCFR node pools (csrc/cit_cfr.h): B per-tree block tables, then one arena
+# of node blocks (CFR_NB node records + CFR_NB game rows) and edge blocks
+# (CFR_EB edge slots) the trees take as they grow.  tests/test_abi.py checks
+# these constants against the library (cit_cfr_block_sizes / cit_cfr_sizes).
+CFR_NB, CFR_EB, CFR_TBL_MAX = 4096, 16384, 1024
+CFR_NODE_BYTES, CFR_EDGE_BYTES, CFR_ARENA_HDR = 168, 48, 64
+
+
+def cfr_nblocks(node_cap):
+    return -(-int(node_cap) // CFR_NB)
+
+
+def cfr_eblocks(edge_cap):
+    return -(-int(edge_cap) // CFR_EB)
+
+
+def cfr_pool_bytes(node_cap, edge_cap):
+    """Bytes per tree ahead of the arena: its node- and edge-block tables (int32, -1 = none)."""
+    return (4 * (cfr_nblocks(node_cap) + cfr_eblocks(edge_cap)) + 15) // 16 * 16
+
+
+def cfr_node_block_bytes():
+    return CFR_NB * (CFR_NODE_BYTES + GAME_BYTES)
+
+
+def cfr_arena_bytes(n_blocks, e_blocks):
+    return CFR_ARENA_HDR + n_blocks * cfr_node_block_bytes() + e_blocks * CFR_EB * CFR_EDGE_BYTES
+
+
+def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
+    """(node records, edge slots, game rows) of tree `lane` as uint8 arrays
+    gathered from its blocks in id order; `read(offset, nbytes)` returns pool
+    bytes as a uint8 ndarray (host pool or device copy)."""
+    import numpy as np
+    per = cfr_pool_bytes(node_cap, edge_cap)
+    nb, eb = cfr_nblocks(node_cap), cfr_eblocks(edge_cap)
+    tbl = np.array(read(lane * per, 4 * (nb + eb))).view("<i4")
+    hdr = np.array(read(B * per, 16)).view("<u4")
+    n_cap = int(hdr[1])
+    node_base = B * per + CFR_ARENA_HDR
+    row_base = node_base + n_cap * CFR_NB * CFR_NODE_BYTES
+    edge_base = row_base + n_cap * CFR_NB * GAME_BYTES
+
+    def held(t):
+        out = []
+        for b in t:
+            if b < 0:
+                break
+            out.append(int(b))
+        return out
+
+    def gather(base, size, blocks):
+        parts = [np.array(read(base + b * size, size)) for b in blocks]
+        return np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+
+    nbl, ebl = held(tbl[:nb]), held(tbl[nb:])
+    nodes = gather(node_base, CFR_NB * CFR_NODE_BYTES, nbl)
+    rows = gather(row_base, CFR_NB * GAME_BYTES, nbl).reshape(-1, GAME_BYTES)
+    edges = gather(edge_base, CFR_EB * CFR_EDGE_BYTES, ebl)
+    return nodes, edges, rows

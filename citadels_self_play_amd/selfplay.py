@@ -94,32 +94,51 @@ def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None):
     return b, chosen, stats, rounds
 
 
+# Arena share of the trees' worst case (node blocks, edge blocks) for batches of
+# >= ARENA_MIN_TREES trees of >= ARENA_MIN_BLOCKS node blocks each: cfr_train(200000)
+# trees average ~1.35 nodes / iteration against pool_caps' 3.5.
+ARENA_FRAC = (0.5, 0.8)
+ARENA_MIN_TREES, ARENA_MIN_BLOCKS = 32, 16
+
+
+def arena_frac_for(B, node_cap):
+    from . import layout as L
+    return ARENA_FRAC if B >= ARENA_MIN_TREES and L.cfr_nblocks(node_cap) >= ARENA_MIN_BLOCKS else None
+
+
 def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_cap=None, max_pool_bytes=None,
-                   log=None):
+                   log=None, arena_frac="auto"):
     """simulate_game (train_from_scratch.py:23-36, pretrain / training=True: the
     search ignores the model) for every seed: random.seed(s), np.random.seed(s),
     create_a_random_game(max_move), run_mccfr(iters, training=True),
     get_all_targets.  Returns (batch, stats, targets dict of device tensors).
 
     Node pools are sized from `iters` (engine.pool_caps: a cfr_train(200000)
-    tree takes ~0.5-1 GB); when the seeds' pools do not fit in
-    `max_pool_bytes` (default: 80 % of the device memory not held by live
-    tensors) the seeds run in consecutive equal chunks and the results are
-    concatenated in seed order (the returned batch is then the last chunk's).
+    tree may grow to ~1.3 GB).  Trees take node blocks from one shared arena
+    as they grow, so a batch of many large trees holds `arena_frac` of their
+    summed worst case (default ARENA_FRAC: ~1.3x the measured mean; a tree
+    that finds the arena exhausted is searched again, bit-identically, in a
+    batch of its own).  When the seeds' pools do not fit in `max_pool_bytes`
+    (default: 80 % of the device memory not held by live tensors) the seeds
+    run in consecutive equal chunks and the results are concatenated in seed
+    order (the returned batch is then the last chunk's).
     targets["terminal"] [B] marks the positions that were already over (the
     reference's run_mccfr raises ValueError on them)."""
-    from . import _lib
+    from .engine import pool_bytes
     if node_cap is None:
         node_cap, ec = pool_caps(iters)
         edge_cap = edge_cap or ec
     edge_cap = edge_cap or 5 * node_cap
     dev = torch.device(device or "cuda")
-    per = _lib.load().cit_cfr_pool_bytes(node_cap, edge_cap)
     if max_pool_bytes is None:
         torch.cuda.empty_cache()                # cached blocks of earlier pools count as free
         max_pool_bytes = int(0.8 * torch.cuda.mem_get_info(dev)[0])
     seeds = np.asarray(seeds, np.int64)
-    chunk = int(max(1, min(len(seeds), max_pool_bytes // max(per, 1))))
+    frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
+    chunk = len(seeds)
+    while chunk > 1 and pool_bytes(chunk, node_cap, edge_cap, frac(chunk)) > max_pool_bytes:
+        per = pool_bytes(chunk, node_cap, edge_cap, frac(chunk)) / chunk
+        chunk = max(1, min(chunk - 1, int(max_pool_bytes // per)))
     n_chunks = -(-len(seeds) // chunk)
     chunk = -(-len(seeds) // n_chunks)           # equal chunks: no short last launch
     parts = []
@@ -128,6 +147,7 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
         if b is not None:
             b.pool = None                      # free the previous chunk's trees
         b = GameBatch(seeds[i:i + chunk], preset=True, device=dev)
+        b.arena_frac = frac(b.B)
         b.random_position(max_move)
         b.seed_numpy()
         term = b.terminal()
@@ -135,8 +155,10 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
         t = b.cfr_targets(stats[:, 0], mode=0)
         t["terminal"] = term
         parts.append((stats, t))
-        if log is not None and len(seeds) > chunk:
-            log("simulate_games: trees %d-%d of %d done" % (i, i + b.B - 1, len(seeds)))
+        if log is not None:
+            used, cap = b.arena_used()
+            log("simulate_games: trees %d-%d of %d done (arena node blocks %d / %d, edge blocks %d / %d)"
+                % (i, i + b.B - 1, len(seeds), used[0], cap[0], used[1], cap[1]))
     if len(parts) == 1:
         return b, parts[0][0], parts[0][1]
     return b, torch.cat([p[0] for p in parts]), concat_targets([p[1] for p in parts], [p[0].shape[0] for p in parts])

@@ -48,7 +48,7 @@ typedef struct CitOption {
   uint64_t x;
 } CitOption;
 
-int cit_abi_version(void);              /* 2: 48-B CfrEdge, 64-bit pool bytes, search flags */
+int cit_abi_version(void);              /* 3: block-allocated node pools (cit_cfr_arena_reset) */
 int cit_game_bytes(void);              /* row width of `games` */
 int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
 int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
@@ -138,12 +138,28 @@ int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1,
 
 /* --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------ */
 
-/* Bytes of node pool per tree (64-bit: a cfr_train(200000) tree needs ~1 GB):
- * node_cap CfrNode (168 B) + edge_cap CfrEdge (48 B), padded to 16 B, +
- * node_cap packed game rows (16-byte aligned).  Opponent nodes reserve 10
- * edges, role-pick nodes 40 slots (10 edges + their [6]-wide regret /
- * strategy columns).  -1 on a bad capacity. */
+/* Node pools.  A pool of B trees = B per-tree block tables
+ * (cit_cfr_pool_bytes each: int32 node-block and edge-block tables for
+ * node_cap / edge_cap) followed by one arena (cit_cfr_arena_bytes(node_blocks,
+ * edge_blocks)): a 64-byte header, node blocks (CFR_NB CfrNode records of
+ * 168 B + CFR_NB packed game rows, 16-byte aligned) and edge blocks (CFR_EB
+ * CfrEdge slots of 48 B).  A tree takes blocks as it grows, so the arena holds
+ * what the trees use, not B worst cases; a tree that reaches its own caps or
+ * finds the arena exhausted stops with CIT_ERR_OVERFLOW (search it again with
+ * more room).  Opponent nodes reserve 10 edges, role-pick nodes 40 slots (10
+ * edges + their [6]-wide regret / strategy columns); a node's edges never
+ * straddle an edge block.  Sizes are 64-bit; -1 on a bad capacity (either
+ * table longer than out[2] of cit_cfr_block_sizes). */
 int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap);
+int64_t cit_cfr_arena_bytes(int node_blocks, int edge_blocks);
+/* out[3] = {CFR_NB nodes per node block, CFR_EB edges per edge block,
+ * table entries a tree may hold}. */
+int cit_cfr_block_sizes(int32_t* out);
+/* Before a search (cit_cfr_decide, or the first cit_cfr_pred_step): every
+ * table entry -1 and the arena empty with node_blocks / edge_blocks capacity.
+ * pool must hold B * cit_cfr_pool_bytes + cit_cfr_arena_bytes(...) bytes. */
+int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                        hipStream_t stream);
 int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */
 
 /* The config-3 position harness: k = random.randint(lo, hi) drawn from the
@@ -173,7 +189,8 @@ int cit_skip_false_choice(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t*
  * games' CPython stream, np_mt/np_idx numpy's global RandomState (seed them
  * with cit_mt_seed(numpy_style=1)).  chosen[l] = the decision; stats[5*l..] =
  * {root node, nodes, edges, carry_out calls, error bits}.  The tree stays in
- * pool (B x cit_cfr_pool_bytes) for inspection / target extraction. */
+ * pool (reset it with cit_cfr_arena_reset first) for inspection / target
+ * extraction. */
 int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
                    int B, int iters, int flags, const int32_t* orig_player, void* pool, int node_cap, int edge_cap,
                    CitOption* optbuf, CitOption* chosen, int32_t* stats, hipStream_t stream);

@@ -88,12 +88,10 @@ WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])
 assert NODE_DT.itemsize == 168 and EDGE_DT.itemsize == 48 and WIDE_DT.itemsize == 3 * 48
 
 
-def cfr_rows_offset(node_cap, edge_cap):
-    return (node_cap * 168 + edge_cap * 48 + 15) // 16 * 16
-
-
-def cfr_pool_bytes(node_cap, edge_cap):
-    return cfr_rows_offset(node_cap, edge_cap) + node_cap * L.GAME_BYTES
+def cfr_pool_bytes(node_cap, edge_cap, B=1):
+    """A host pool of B trees with the worst-case arena (layout.cfr_* / cit_cfr.h)."""
+    return B * L.cfr_pool_bytes(node_cap, edge_cap) + \
+        L.cfr_arena_bytes(B * L.cfr_nblocks(node_cap), B * L.cfr_eblocks(edge_cap))
 
 
 def node_arrays(nodes, edges, n):
@@ -120,7 +118,7 @@ class HostCfr:
         self.npmt = np.zeros((L.MT_N, B), np.uint32)
         self.npidx = np.zeros(B, np.uint32)
         lib().cith_mt_seed(_p(self.npmt), _p(self.npidx), C.c_int(B), _p(hb.seeds), C.c_int(1))
-        self.pool = np.zeros(B * cfr_pool_bytes(node_cap, edge_cap), np.uint8)
+        self.pool = np.zeros(cfr_pool_bytes(node_cap, edge_cap, B), np.uint8)
         self.optbuf = np.zeros((B, 512, 16), np.uint8)
 
     def advance(self, lo, hi):
@@ -130,8 +128,15 @@ class HostCfr:
                                   C.c_int(hi), _p(steps))
         return steps
 
+    def reset(self):
+        """Empty block tables and arena (before each search; cfr_pred resumptions keep them)."""
+        B = self.hb.B
+        lib().cith_cfr_arena_reset(_p(self.pool), C.c_int(B), C.c_int(self.node_cap), C.c_int(self.edge_cap),
+                                   C.c_int(B * L.cfr_nblocks(self.node_cap)), C.c_int(B * L.cfr_eblocks(self.edge_cap)))
+
     def decide(self, iters, flags=0):
         hb = self.hb
+        self.reset()
         chosen = np.zeros((hb.B, 16), np.uint8)
         stats = np.zeros((hb.B, 5), np.int32)
         lib().cith_cfr_decide(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(self.npmt), _p(self.npidx), _p(hb.seer),
@@ -140,14 +145,9 @@ class HostCfr:
         return chosen, stats
 
     def tree(self, l):
-        per = cfr_pool_bytes(self.node_cap, self.edge_cap)
-        base = self.pool[l * per:(l + 1) * per]
-        nb, eb = self.node_cap * 168, self.edge_cap * 48
-        nodes = base[:nb].view(NODE_DT)
-        edges = base[nb:nb + eb].view(EDGE_DT)
-        ro = cfr_rows_offset(self.node_cap, self.edge_cap)
-        rows = base[ro:ro + self.node_cap * L.GAME_BYTES].reshape(self.node_cap, L.GAME_BYTES)
-        return nodes, edges, rows
+        nodes, edges, rows = L.cfr_tree_bytes(lambda o, n: self.pool[o:o + n], self.hb.B, l, self.node_cap,
+                                              self.edge_cap)
+        return nodes.view(NODE_DT), edges.view(EDGE_DT), rows
 
 
 def encode_games(hb, pid=-1):
@@ -174,6 +174,7 @@ def cfr_pred(cf, iters, max_depth, mlp):
     feat = np.zeros((B, 418), np.float32)
     chosen = np.zeros((B, 16), np.uint8)
     rounds = 0
+    cf.reset()
     while True:
         w = lib().cith_cfr_pred_step(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(cf.npmt), _p(cf.npidx), _p(hb.seer),
                                      C.c_int(B), C.c_int(iters), C.c_int(max_depth), _p(cf.pool),

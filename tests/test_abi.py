@@ -32,16 +32,34 @@ def test_layout_matches(lib):
     assert list(out[:n]) == L.expected_layout()
     assert lib.cit_game_bytes() == L.GAME_BYTES
     assert lib.cit_seer_scratch_words() == L.SEER_MAX
-    assert lib.cit_abi_version() == 2
+    assert lib.cit_abi_version() == 3
 
 
-def test_cfr_pool_bytes_64bit(lib):
-    # cfr_train(200000) pools exceed 2 GiB per tree (round 1 returned -1 there)
-    nc, ec = 500_256, 5 * 500_256
-    assert lib.cit_cfr_pool_bytes(nc, ec) == (nc * 168 + ec * 48 + 15) // 16 * 16 + nc * L.GAME_BYTES
-    assert lib.cit_cfr_pool_bytes(3, 5) % 16 == 0   # rows (and the next tree's pool) 16-byte aligned
-    assert lib.cit_cfr_pool_bytes(4_000_000, 20_000_000) > 2 ** 31
+def test_cfr_pool_layout(lib):
+    # per-tree block tables + one 64-bit arena (csrc/cit_cfr.h; layout.cfr_*)
+    sizes = (C.c_int32 * 3)()
+    assert lib.cit_cfr_block_sizes(sizes) == 0
+    assert list(sizes) == [L.CFR_NB, L.CFR_EB, L.CFR_TBL_MAX]
+    out = (C.c_int * 8)()
+    h = __import__("tests.hostcheck", fromlist=["lib"]).lib()
+    assert h.cith_cfr_sizes(out) == 5
+    assert list(out[:5]) == [L.CFR_NODE_BYTES, L.CFR_EDGE_BYTES, lib.cit_cfr_opt_cap(), L.CFR_NB, L.CFR_EB]
+    nc, ec = 700_512, 4 * 700_512 + 4096                      # pool_caps(200000)
+    assert lib.cit_cfr_pool_bytes(nc, ec) == L.cfr_pool_bytes(nc, ec) == (4 * (172 + 172) + 15) // 16 * 16
+    assert lib.cit_cfr_pool_bytes(3, 5) % 16 == 0             # the next tree's tables 16-byte aligned
+    assert lib.cit_cfr_arena_bytes(172 * 300, 172 * 300) == L.cfr_arena_bytes(172 * 300, 172 * 300) > 2 ** 38
     assert lib.cit_cfr_pool_bytes(0, 10) == -1
+    assert lib.cit_cfr_pool_bytes(L.CFR_TBL_MAX * L.CFR_NB + 1, 10) == -1   # table longer than a tree may hold
+    assert lib.cit_cfr_arena_bytes(-1, 0) == -1
+    assert lib.cit_cfr_arena_reset(None, 4, 16, 16, 1, 1, None) == -1
+
+
+def test_arena_blocks():
+    from citadels_self_play_amd.engine import arena_blocks, pool_bytes
+    assert arena_blocks(10, 700_512, 2_806_144) == (1720, 1720)
+    assert arena_blocks(10, 700_512, 2_806_144, (0.5, 0.8)) == (860, 1376)
+    assert arena_blocks(1, 100, 500, 0.1) == (1, 1)           # never below one tree's worst case
+    assert pool_bytes(2, 100, 500) == 2 * 16 + L.cfr_arena_bytes(2, 2)
 
 
 def test_bad_args_rejected(lib):

@@ -20,6 +20,7 @@ pytestmark = pytest.mark.gpu
 
 def test_gpu_shard_invariance_simulate_games():
     from citadels_self_play_amd import selfplay
+    from citadels_self_play_amd.engine import pool_bytes
     n, iters = 24, 2000
     whole_b, whole_stats, whole_t = selfplay.simulate_games(selfplay.shard(n, 4242, 0, 1), iters)
     parts = [selfplay.simulate_games(selfplay.shard(n, 4242, r, 2), iters) for r in range(2)]
@@ -30,8 +31,7 @@ def test_gpu_shard_invariance_simulate_games():
         assert torch.equal(t[k].cpu(), whole_t[k].cpu()), k
     # and in memory-bounded chunks (3 trees per chunk) within one rank
     cb, cstats, ct = selfplay.simulate_games(selfplay.shard(n, 4242, 0, 1), iters,
-                                             max_pool_bytes=3 * whole_b.lib.cit_cfr_pool_bytes(whole_b.node_cap,
-                                                                                                whole_b.edge_cap))
+                                             max_pool_bytes=pool_bytes(3, whole_b.node_cap, whole_b.edge_cap))
     assert torch.equal(cstats.cpu(), whole_stats.cpu())
     for k in ("meta", "feat", "value", "dist", "opt_feat", "counts"):
         assert torch.equal(ct[k].cpu(), whole_t[k].cpu()), k

@@ -42,7 +42,8 @@ struct CfrNode {                       // 168 B
   int8_t player, gs_state;
   uint8_t flags;
   int8_t winner;
-  uint8_t pad[6];
+  int16_t sib;                         // index among the parent's children (-1: root)
+  uint8_t pad[4];
   double nv[6], wp[6], pred[6];
 };
 // An edge = (option, child) and the parent's regret / strategy / cumulative
@@ -69,9 +70,12 @@ static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
 // averages ~270k nodes against a ~650k-node maximum):
 //   per tree l (cfr_pool_bytes each): int32 node-block table [nblocks(node_cap)]
 //     | int32 edge-block table [eblocks(edge_cap)] | pad to 16 B
-//   arena (at B * cfr_pool_bytes): CfrArena header (64 B) | node records
-//     [n_cap blocks][CFR_NB] | node game rows [n_cap blocks][CFR_NB] (16-byte
+//   arena (at B * cfr_pool_bytes): CfrArena header (64 B) | free-block rings
+//     uint32 [n_cap] + [e_cap] (padded to 16 B) | node records [n_cap
+//     blocks][CFR_NB] | node game rows [n_cap blocks][CFR_NB] (16-byte
 //     aligned, copied as 16-byte words) | edges [e_cap blocks][CFR_EB]
+// A block is taken from its free ring (blocks released by finished trees,
+// cit_cfr_arena_release) or, when that is empty, from the never-used rest.
 // Node id n lives in block nbt[n >> CFR_NB_SHIFT] at slot n & (CFR_NB - 1);
 // edge index e likewise through ebt.  An edge run (a node's children) never
 // straddles an edge block.  Sizes are 64-bit.
@@ -81,8 +85,9 @@ static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
 #define CFR_EB (1 << CFR_EB_SHIFT)            // edge slots per block: 768 KB
 #define CFR_TBL_MAX 1024                      // table entries a device tree keeps in LDS
 struct CfrArena {                             // 64 B, written by cit_cfr_arena_reset
-  uint32_t n_next, n_cap, e_next, e_cap;      // blocks handed out / capacity
-  uint32_t pad[12];
+  uint32_t n_next, n_cap, e_next, e_cap;      // never-used blocks handed out / capacity
+  uint32_t n_head, n_tail, e_head, e_tail;    // free rings: taken / released counts (mod cap)
+  uint32_t pad[8];
 };
 static_assert(sizeof(CfrArena) == 64, "CfrArena layout");
 
@@ -118,8 +123,9 @@ CIT_HD int64_t cfr_pool_bytes(int node_cap, int edge_cap) {   // per tree: its t
   return ((int64_t)4 * (cfr_nblocks(node_cap) + cfr_eblocks(edge_cap)) + 15) & ~(int64_t)15;
 }
 CIT_HD int64_t cfr_node_block_bytes() { return (int64_t)CFR_NB * (int64_t)(sizeof(CfrNode) + CIT_GAME_BYTES); }
+CIT_HD int64_t cfr_ring_bytes(int64_t n_blocks, int64_t e_blocks) { return (4 * (n_blocks + e_blocks) + 15) & ~(int64_t)15; }
 CIT_HD int64_t cfr_arena_bytes(int n_blocks, int e_blocks) {
-  return (int64_t)sizeof(CfrArena) + (int64_t)n_blocks * cfr_node_block_bytes() +
+  return (int64_t)sizeof(CfrArena) + cfr_ring_bytes(n_blocks, e_blocks) + (int64_t)n_blocks * cfr_node_block_bytes() +
          (int64_t)e_blocks * CFR_EB * (int64_t)sizeof(CfrEdge);
 }
 // Binds tree l of a B-tree pool; the arena's capacities come from its header.
@@ -132,8 +138,8 @@ CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, int B, long l, int node_cap
   T.ebt = T.ebt_hbm;
   uint8_t* a = pool + per * (int64_t)B;
   T.arena = reinterpret_cast<CfrArena*>(a);
-  int64_t ncap = T.arena->n_cap;
-  T.node_base = a + sizeof(CfrArena);
+  int64_t ncap = T.arena->n_cap, ecap = T.arena->e_cap;
+  T.node_base = a + sizeof(CfrArena) + cfr_ring_bytes(ncap, ecap);
   T.row_base = T.node_base + ncap * CFR_NB * (int64_t)sizeof(CfrNode);
   T.edge_base = T.row_base + ncap * CFR_NB * (int64_t)CIT_GAME_BYTES;
   T.node_cap = node_cap;
@@ -233,17 +239,38 @@ CIT_HD CitGame& cfr_w(const CfrTree& T, int which) { return which ? *T.w1 : *T.w
 CIT_HD CitOpt* cfr_lbuf(const CfrTree& T) { return T.lbuf; }
 CIT_HD uint8_t* cfr_tmp(const CfrTree& T) { return T.tmp; }
 #endif
-// One block from an arena counter (lane 0's atomic on the device); -1 when
-// the arena is full.
-CIT_HD int cfr_take_block(uint32_t* next, uint32_t cap) {
+// One block for a tree (edge = 0: a node block, 1: an edge block): lane 0
+// takes the next entry of the free ring, or a never-used block when the ring
+// is empty; -1 when the arena is full.  Takes run concurrently (atomics);
+// releases only between launches, so the ring's tail is fixed meanwhile and
+// a head that overshoots it is pulled back by the next release.
+CIT_HD int cfr_take_block(CfrArena* A, int edge) {
+  uint32_t* ring = reinterpret_cast<uint32_t*>(A + 1) + (edge ? A->n_cap : 0);
+  uint32_t cap = edge ? A->e_cap : A->n_cap;
+  uint32_t* head = edge ? &A->e_head : &A->n_head;
+  uint32_t tail = edge ? A->e_tail : A->n_tail;
+  uint32_t* next = edge ? &A->e_next : &A->n_next;
+  int r = -1;
 #if CIT_WAVE
-  uint32_t v = 0;
-  if (__lane_id() == 0) v = atomicAdd(next, 1u);
-  v = cfr_u(v);
+  if (__lane_id() == 0) {
+    if (*head < tail) {
+      uint32_t h = atomicAdd(head, 1u);
+      if (h < tail) r = (int)ring[h % cap];
+    }
+    if (r < 0) {
+      uint32_t v = atomicAdd(next, 1u);
+      r = v < cap ? (int)v : -1;
+    }
+  }
+  r = cfr_u(r);
 #else
-  uint32_t v = (*next)++;
+  if (*head < tail) r = (int)ring[(*head)++ % cap];
+  if (r < 0) {
+    uint32_t v = (*next)++;
+    r = v < cap ? (int)v : -1;
+  }
 #endif
-  return v < cap ? (int)v : -1;
+  return r;
 }
 
 // The block tables: LDS (fixed addresses) in a device search, else the pool's.
@@ -572,7 +599,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
   int id = T.n_nodes;
   if ((id & (CFR_NB - 1)) == 0) {       // the first node of a new block
-    int b = cfr_take_block(&cfr_glb(T.arena)->n_next, cfr_glb(T.arena)->n_cap);
+    int b = cfr_take_block(cfr_glb(T.arena), 0);
     if (b < 0) { T.err |= CIT_ERR_OVERFLOW; return -1; }
     cfr_nbt(T)[id >> CFR_NB_SHIFT] = b;
   }
@@ -586,7 +613,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
     hw[2] = 0;                                   // n_children, edge_cap
     hw[3] = (uint32_t)(uint16_t)depth | ((uint32_t)(uint8_t)w.gs_pid << 16) | ((uint32_t)w.gs_state << 24);
     hw[4] = (uint32_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0)) |
-            ((uint32_t)(uint8_t)w.winner << 8);
+            ((uint32_t)(uint8_t)w.winner << 8) | 0xffff0000u;   // sib = -1 until the parent links it
     hw[5] = 0;
     const int l = CFR_LANE;
     uint32_t v = 0;
@@ -603,6 +630,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   N.gs_state = (int8_t)w.gs_state;
   N.flags = (uint8_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0));
   N.winner = w.winner;
+  N.sib = -1;
   for (int k = 0; k < 6; k++) N.nv[k] = N.wp[k] = N.pred[k] = 0.0;
 #endif
   copy_row(T, row_of(T, id), w_row(T, which));
@@ -615,7 +643,7 @@ CIT_HD int alloc_edges(CfrTree& T, int n) {
   if ((f & (CFR_EB - 1)) + n > CFR_EB) f = (f | (CFR_EB - 1)) + 1;
   if (f + n > T.edge_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
   while (((f + n - 1) >> CFR_EB_SHIFT) >= T.n_eblk) {
-    int b = cfr_take_block(&cfr_glb(T.arena)->e_next, cfr_glb(T.arena)->e_cap);
+    int b = cfr_take_block(cfr_glb(T.arena), 1);
     if (b < 0) { T.err |= CIT_ERR_OVERFLOW; return -1; }
     cfr_ebt(T)[T.n_eblk++] = b;
   }
@@ -661,6 +689,7 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
     int c = cfr_u(cfr_node(T, 1, n, depth, 0));
     if (c < 0) return;
     init_edge((*cfr_edge(T, f + r)), last, c);
+    cfr_node(T, c).sib = (int16_t)r;
     cfr_node(T, n).n_children = (int16_t)(r + 1);
   }
 }
@@ -701,6 +730,7 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
     int c = cfr_u(cfr_node(T, 1, n, depth, 0));
     if (c < 0) return;
     init_edge((*cfr_edge(T, f + i)), o, c);
+    cfr_node(T, c).sib = (int16_t)i;
     cfr_node(T, n).n_children = (int16_t)(i + 1);
   }
 }
@@ -736,6 +766,7 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
   int c = cfr_u(cfr_node(T, 1, n, N.depth + 1, 0));
   if (c < 0) return;
   init_edge((*cfr_edge(T, cfr_node(T, n).first_edge + cfr_node(T, n).n_children)), key, c);
+  cfr_node(T, c).sib = cfr_node(T, n).n_children;
   cfr_node(T, n).n_children++;
 }
 
@@ -912,17 +943,53 @@ CIT_HD void cfr_backprop_arr(CfrTree& T, int n, const double* rw, bool model) {
 }
 
 // ---------------------------------------------------------------- drivers
-// cfr_train(iters) on the game in working row 0 (the root's game:
+// cfr_train(iters) (:187-205) on the game in working row 0 (the root's game:
 // skip_false_choice mutates it, as the reference mutates the game passed to
-// CFRNode).  Returns the root id.
-CIT_HD int cfr_train(CfrTree& T_in, int iters, bool root_skipped = false) {
+// CFRNode), as resumable slices (the tree queue of simulate_games): phase
+// CP_INIT builds the root; CP_RUN resumes iteration S.it at
+// node S.cur.  A slice stops at an iteration boundary, after at least one
+// iteration, once its budget is spent (device: `ticks` of the 100 MHz wall
+// clock since `t0`; host: `iters_left` iterations), returning 1; 0 when the
+// tree is done (S.phase == CP_DONE; S.root as cfr_train returns it).  The
+// tree, streams and counters come out bit-identical to one cfr_train call.
+struct CfrBudget {
+  uint64_t t0, ticks;
+  int iters_left;
+};
+CIT_HD bool cfr_budget_spent(CfrBudget& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return b.ticks && wall_clock64() - b.t0 >= b.ticks;
+#else
+  return b.iters_left > 0 && --b.iters_left == 0;
+#endif
+}
+CIT_HD int cfr_train_slice(CfrTree& T_in, CfrState& S_in, int iters, bool root_skipped, CfrBudget& bud) {
   CfrTree& T = CFR_T(T_in);
-  int root = cfr_u(cfr_node(T, 0, -1, 0, root_skipped ? 1 : 0));
-  if (root < 0 || T.err) return root;
-  if (cfr_node(T, root).flags & NF_TERMINAL) return root;
-  cfr_expand(T, root);
-  int n = root;
-  for (int it = 0; it < iters && !T.err; it++) {
+  CfrState& S = CFR_S(S_in);
+  if (cfr_u(S.phase) == CP_DONE) return 0;
+  int root, n, it;
+  if (cfr_u(S.phase) == CP_INIT) {
+    root = cfr_u(cfr_node(T, 0, -1, 0, root_skipped ? 1 : 0));
+    S.root = root;
+    S.phase = CP_DONE;
+    if (root < 0 || T.err) return 0;
+    if (cfr_node(T, root).flags & NF_TERMINAL) return 0;
+    cfr_expand(T, root);
+    S.phase = CP_RUN;
+    n = root;
+    it = 0;
+  } else {
+    root = cfr_u(S.root);
+    n = cfr_u(S.cur);
+    it = cfr_u(S.it);
+  }
+  int first = it;
+  for (; it < iters && !T.err; it++) {
+    if (it > first && cfr_budget_spent(bud)) {
+      S.cur = n;
+      S.it = it;
+      return 1;
+    }
     cfr_update_strategy(T, n);
     int a = cfr_u(cfr_choose(T, n));
     if (T.err) break;
@@ -938,7 +1005,18 @@ CIT_HD int cfr_train(CfrTree& T_in, int iters, bool root_skipped = false) {
     }
   }
   if (!T.err) cfr_update_strategy(T, root);
-  return root;
+  S.phase = CP_DONE;
+  return 0;
+}
+
+// The whole search in one call.  Returns the root id.
+CIT_HD int cfr_train(CfrTree& T, int iters, bool root_skipped = false) {
+  CfrState S_local;
+  CfrState& S = CFR_S(S_local);
+  S.phase = CP_INIT;
+  CfrBudget b = {0, 0, 0};
+  cfr_train_slice(T, S_local, iters, root_skipped, b);
+  return cfr_u(S.root);
 }
 
 // action_choice(live=True) at the root (:67-91; game.py:312-317 for a role pick).
@@ -1090,17 +1168,28 @@ CIT_HD bool cfr_is_target(const CfrTree& T, int n) {
   return s >= CFR_TARGET_THRESHOLD;
 }
 
-// Pre-order successor within the subtree of `top` through parent links (-1
-// after its last node).
-CIT_HD int cfr_preorder_next(const CfrTree& T, int n, int top) {
+// Pre-order successor within the subtree of `top` through parent links and
+// sibling indices (-1 after its last node).  With `prune`, the subtree of a
+// node visited fewer than CFR_TARGET_THRESHOLD times is skipped: it holds no
+// target when visit counts only grow towards the root (trees searched without
+// a model: every backprop adds its reward to the whole path).
+CIT_HD int cfr_preorder_next(const CfrTree& T, int n, int top, bool prune = false) {
   const CfrNode& N = cfr_node(T, n);
-  if (N.n_children > 0) return (*cfr_edge(T, N.first_edge)).child;
+  if (N.n_children > 0) {
+    bool skip = false;
+    if (prune) {
+      double s = 0.0;
+      for (int k = 0; k < 6; k++) s += N.nv[k];
+      skip = s < CFR_TARGET_THRESHOLD;
+    }
+    if (!skip) return (*cfr_edge(T, N.first_edge)).child;
+  }
   for (;;) {
-    int p = cfr_node(T, n).parent;
+    const CfrNode& M = cfr_node(T, n);
+    int p = M.parent;
     if (n == top || p < 0) return -1;
     const CfrNode& P = cfr_node(T, p);
-    int j = 0;
-    while (j < P.n_children && (*cfr_edge(T, P.first_edge + j)).child != n) j++;
+    int j = M.sib;
     if (j + 1 < P.n_children) return (*cfr_edge(T, P.first_edge + j + 1)).child;
     n = p;
   }
@@ -1115,14 +1204,16 @@ CIT_HD CfrTree cfr_tree_view(uint8_t* pool, int B, long l, int node_cap, int edg
 
 // Target modes: CFR_TGT_TREE = get_all_targets over the tree; CFR_TGT_ROOT =
 // run_utils.create_target_strategy + encode_options_from_node at the root only
-// (run_utils.py:89-109; generate_test_data.py:18-26), no threshold.
-enum { CFR_TGT_TREE = 0, CFR_TGT_ROOT = 1 };
+// (run_utils.py:89-109; generate_test_data.py:18-26), no threshold.  Flag
+// CFR_TGT_PRUNE (with TREE): the trees were searched without a model, so the
+// walk skips subtrees under the visit threshold (cfr_preorder_next).
+enum { CFR_TGT_TREE = 0, CFR_TGT_ROOT = 1, CFR_TGT_PRUNE = 2 };
 
 CIT_HD bool cfr_target_sel(const CfrTree& T, int n, int mode) {
-  return mode == CFR_TGT_ROOT ? cfr_node(T, n).n_children > 0 : cfr_is_target(T, n);
+  return (mode & CFR_TGT_ROOT) ? cfr_node(T, n).n_children > 0 : cfr_is_target(T, n);
 }
 CIT_HD int cfr_target_next(const CfrTree& T, int n, int top, int mode) {
-  return mode == CFR_TGT_ROOT ? -1 : cfr_preorder_next(T, n, top);
+  return (mode & CFR_TGT_ROOT) ? -1 : cfr_preorder_next(T, n, top, (mode & CFR_TGT_PRUNE) != 0);
 }
 
 // Number of targets and of their children (option rows).

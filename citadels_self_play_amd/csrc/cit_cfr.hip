@@ -161,6 +161,92 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   }
 }
 
+// One slice of cfr_train per tree (the tree queue of simulate_games): the
+// tree resumes from its CfrState and runs until `ticks` of the wall clock
+// have passed (then lane 0 adds 1 to *running) or it is done (then as
+// k_cfr_decide: live choice, root game back into games[l], chosen, stats).
+__global__ __launch_bounds__(64) void k_cfr_train_slice(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
+                                                        uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
+                                                        const int32_t* orig, uint8_t* pool, int node_cap, int edge_cap,
+                                                        CitOpt* optbuf, CfrState* state, uint64_t ticks,
+                                                        CitOpt* chosen, int32_t* stats, int32_t* running) {
+  long l = blockIdx.x;
+  if (l >= B) return;
+  CfrBudget bud;
+  bud.t0 = wall_clock64();
+  bud.ticks = ticks;
+  bud.iters_left = 0;
+  CfrState& S = cfr_ls.S;
+  S = state[l];
+  if (S.phase == CP_DONE) return;
+  CfrTree& T = cfr_ls.T;
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf);
+  if (S.phase == CP_INIT) {
+    T.n_nodes = T.n_edges = 0;
+    T.err = 0;
+    T.carry_outs = 0;
+    copy_row(T, cfr_ls.w[0], games + l * ROW_W);
+    T.orig = orig ? orig[l] : cfr_w(T, 0).gs_pid;
+    S.orig = T.orig;
+  } else {
+    cfr_state_load(T, S);
+    tables_load(T, T.n_nodes, T.n_edges);
+  }
+  int r = cfr_u(cfr_train_slice(T, S, iters, (flags & CIT_CFR_ROOT_SKIPPED) != 0, bud));
+  int root = cfr_u(S.root);
+  CitOpt c = mk(O_NUM_NAMES, 0);
+  if (!r) {
+    if (root >= 0 && !T.err) c = cfr_uopt(cfr_live_choice(T, root));
+    if (root >= 0) copy_row(T, games + l * ROW_W, row_of(T, root));
+  }
+  cfr_state_save(T, S);
+  tables_store(T);
+  mt_stage_out(cfr_ls.py, mt, B, l);
+  mt_stage_out(cfr_ls.np, npmt, B, l);
+  if (threadIdx.x == 0) {
+    state[l] = S;
+    idx[l] = T.py.pos;
+    npidx[l] = T.np.pos;
+    if (r) {
+      atomicAdd(running, 1);
+    } else {
+      chosen[l] = c;
+      stats[5 * l + 0] = root;
+      stats[5 * l + 1] = T.n_nodes;
+      stats[5 * l + 2] = T.n_edges;
+      stats[5 * l + 3] = (int)T.carry_outs;
+      stats[5 * l + 4] = (int)T.err;
+    }
+  }
+}
+
+// Releasing trees' blocks (between launches): first pull each ring's head
+// back to its tail (takes past an empty ring overshoot it), then one
+// workgroup per released tree appends its blocks to the rings and clears its
+// tables.
+__global__ void k_arena_clamp(CfrArena* a) {
+  if (threadIdx.x == 0) {
+    if (a->n_head > a->n_tail) a->n_head = a->n_tail;
+    if (a->e_head > a->e_tail) a->e_head = a->e_tail;
+  }
+}
+__global__ void k_arena_release(int32_t* tables, long per_words, int nb, int eb, CfrArena* a, const int32_t* lanes) {
+  int32_t* t = tables + (long)lanes[blockIdx.x] * per_words;
+  uint32_t* ring = reinterpret_cast<uint32_t*>(a + 1);
+  for (int i = threadIdx.x; i < nb + eb; i += blockDim.x) {
+    int b = t[i];
+    if (b < 0) continue;
+    if (i < nb) {
+      uint32_t pos = atomicAdd(&a->n_tail, 1u);
+      ring[pos % a->n_cap] = (uint32_t)b;
+    } else {
+      uint32_t pos = atomicAdd(&a->e_tail, 1u);
+      ring[a->n_cap + pos % a->e_cap] = (uint32_t)b;
+    }
+    t[i] = -1;
+  }
+}
+
 // A pool before its trees start: every block-table entry -1, the arena
 // header with no blocks handed out and the given capacities.
 __global__ void k_arena_reset(int32_t* tables, long n_words, CfrArena* a, uint32_t n_cap, uint32_t e_cap) {
@@ -205,6 +291,17 @@ int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_
                      n_words, reinterpret_cast<CfrArena*>(a), (uint32_t)node_blocks, (uint32_t)edge_blocks);
   CHECK_LAUNCH();
 }
+int cit_cfr_arena_release(void* pool, int B, int node_cap, int edge_cap, const int32_t* lanes, int n_lanes,
+                          hipStream_t stream) {
+  if (!pool || B <= 0 || n_lanes < 0 || (n_lanes && !lanes) || cit_cfr_pool_bytes(node_cap, edge_cap) < 0) return -1;
+  int64_t per = cfr_pool_bytes(node_cap, edge_cap);
+  CfrArena* a = reinterpret_cast<CfrArena*>((uint8_t*)pool + per * (int64_t)B);
+  hipLaunchKernelGGL(k_arena_clamp, dim3(1), dim3(64), 0, stream, a);
+  if (n_lanes)
+    hipLaunchKernelGGL(k_arena_release, dim3(n_lanes), dim3(256), 0, stream, (int32_t*)pool, (long)(per / 4),
+                       cfr_nblocks(node_cap), cfr_eblocks(edge_cap), a, lanes);
+  CHECK_LAUNCH();
+}
 int cit_cfr_opt_cap(void) { return CFR_OPT_CAP; }
 
 int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
@@ -219,6 +316,19 @@ int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt,
 }
 
 int cit_cfr_state_bytes(void) { return (int)sizeof(CfrState); }
+
+int cit_cfr_train_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                        int B, int iters, int flags, const int32_t* orig_player, void* pool, int node_cap, int edge_cap,
+                        CitOption* optbuf, void* state, int64_t slice_ticks, CitOption* chosen, int32_t* stats,
+                        int32_t* running, hipStream_t stream) {
+  if (B <= 0 || iters < 0 || slice_ticks < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt ||
+      !mt_idx || !np_mt || !np_idx || !seer || !pool || !optbuf || !state || !chosen || !stats || !running)
+    return -1;
+  hipLaunchKernelGGL(k_cfr_train_slice, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
+                     seer, B, iters, flags, orig_player, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
+                     (CfrState*)state, (uint64_t)slice_ticks, (CitOpt*)chosen, stats, running);
+  CHECK_LAUNCH();
+}
 
 int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
                       int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,

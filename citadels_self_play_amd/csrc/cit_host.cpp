@@ -238,6 +238,87 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
   free(w1);
 }
 
+// cit_cfr_train_slice with an iteration budget per slice (slice_iters, 0 =
+// none) instead of the wall clock; st = B CfrState (zero before the first
+// call).  Returns the number of trees still running.
+int cith_cfr_train_slice(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx, uint64_t* seer,
+                         int B, int iters, int flags, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
+                         CfrState* st, int slice_iters, CitOpt* chosen, int* stats) {
+  CitGame* w0 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
+  CitGame* w1 = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
+  uint8_t tmp[CIT_SAMPLE_SCRATCH];
+  CitOpt lbuf[CFR_LBUF];
+  int running = 0;
+  for (int l = 0; l < B; l++) {
+    CfrState& S = st[l];
+    if (S.phase == CP_DONE) continue;
+    CfrTree T;
+    cfr_tree_bind(T, pool, B, l, node_cap, edge_cap);
+    T.n_eblk = 0;
+    T.training = false;
+    T.py = lane_rng(mt, idx, B, l);
+    T.np = lane_rng(npmt, npidx, B, l);
+    T.seer = seer + (long)l * CIT_SEER_MAX;
+    T.optbuf = optbuf + (long)l * CFR_OPT_CAP;
+    T.w0 = w0;
+    T.w1 = w1;
+    T.tmp = tmp;
+    T.lbuf = lbuf;
+    if (S.phase == CP_INIT) {
+      T.n_nodes = T.n_edges = 0;
+      T.err = 0;
+      T.carry_outs = 0;
+      memcpy(w0, &g[l], CIT_GAME_BYTES);
+      T.orig = S.orig = g[l].gs_pid;
+    } else {
+      cfr_state_load(T, S);
+    }
+    CfrBudget bud = {0, 0, slice_iters};
+    int r = cfr_train_slice(T, S, iters, (flags & 1) != 0, bud);
+    cfr_state_save(T, S);
+    idx[l] = T.py.pos;
+    npidx[l] = T.np.pos;
+    if (r) {
+      running++;
+      continue;
+    }
+    int root = S.root;
+    CitOpt c = mk(O_NUM_NAMES, 0);
+    if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
+    chosen[l] = c;
+    if (root >= 0) memcpy(&g[l], row_of(T, root), CIT_GAME_BYTES);
+    idx[l] = T.py.pos;
+    npidx[l] = T.np.pos;
+    stats[5 * l + 0] = root;
+    stats[5 * l + 1] = T.n_nodes;
+    stats[5 * l + 2] = T.n_edges;
+    stats[5 * l + 3] = (int)T.carry_outs;
+    stats[5 * l + 4] = (int)T.err;
+  }
+  free(w0);
+  free(w1);
+  return running;
+}
+
+// cit_cfr_arena_release: the blocks of trees lanes[0..n) back to the rings.
+void cith_cfr_arena_release(uint8_t* pool, int B, int node_cap, int edge_cap, const int* lanes, int n) {
+  int64_t per = cfr_pool_bytes(node_cap, edge_cap);
+  CfrArena* a = reinterpret_cast<CfrArena*>(pool + per * (int64_t)B);
+  uint32_t* ring = reinterpret_cast<uint32_t*>(a + 1);
+  if (a->n_head > a->n_tail) a->n_head = a->n_tail;
+  if (a->e_head > a->e_tail) a->e_head = a->e_tail;
+  int nb = cfr_nblocks(node_cap), eb = cfr_eblocks(edge_cap);
+  for (int k = 0; k < n; k++) {
+    int32_t* t = reinterpret_cast<int32_t*>(pool + per * (int64_t)lanes[k]);
+    for (int i = 0; i < nb + eb; i++) {
+      if (t[i] < 0) continue;
+      if (i < nb) ring[a->n_tail++ % a->n_cap] = (uint32_t)t[i];
+      else ring[a->n_cap + a->e_tail++ % a->e_cap] = (uint32_t)t[i];
+      t[i] = -1;
+    }
+  }
+}
+
 void cith_encode_games(const CitGame* g, int B, int pid, float* out) {
   for (int l = 0; l < B; l++) cit_encode_game(g[l], out + (long)l * CIT_FEAT, pid);
 }

@@ -139,7 +139,7 @@ extern "C" {
 
 int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
                          int32_t* counts, hipStream_t stream) {
-  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !counts || mode < 0 || mode > 1) return -1;
+  if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !counts || mode < 0 || mode > 3) return -1;
   hipLaunchKernelGGL(k_cfr_target_count, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap,
                      edge_cap, roots, mode, counts);
   CHECK_LAUNCH();
@@ -149,7 +149,7 @@ int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t
                     uint32_t* mt_idx, const int32_t* offsets, int32_t* meta, float* feat, double* value, double* dist,
                     float* opt_feat, hipStream_t stream) {
   if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !mt || !mt_idx || !offsets || mode < 0 ||
-      mode > 1)
+      mode > 3)
     return -1;
   hipLaunchKernelGGL(k_cfr_targets, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap, edge_cap,
                      roots, mode, mt, mt_idx, offsets, meta, feat, value, dist, opt_feat);

@@ -22,7 +22,7 @@ from . import layout as L
 
 NODE_DT = np.dtype([("parent", "<i4"), ("first_edge", "<i4"), ("n_children", "<i2"), ("edge_cap", "<i2"),
                     ("depth", "<i2"), ("player", "i1"), ("gs_state", "i1"), ("flags", "u1"), ("winner", "i1"),
-                    ("pad", "u1", 6), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
+                    ("sib", "<i2"), ("pad", "u1", 4), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
 ERR_OVERFLOW = 0x1         # CIT_ERR_OVERFLOW (csrc/cit_core.h)
 EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8"), ("S", "<f8"), ("CS", "<f8")])
 WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])   # role-pick columns (csrc/cit_cfr.h)
@@ -228,6 +228,7 @@ class GameBatch:
 
     def _cfr_decide(self, iters, node_cap, edge_cap, flags=0, orig=None):
         self._pool(node_cap, edge_cap)
+        self._model_tree = False
         node_cap, edge_cap = self.node_cap, self.edge_cap
         o = self._orig(orig)
         chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
@@ -318,6 +319,9 @@ class GameBatch:
 
     def _cfr_targets(self, roots, mode):
         d = self.device
+        if mode == 0 and getattr(self, "_model_tree", True) is False:
+            mode = 2                                  # CFR_TGT_PRUNE: searched without a model
+
         counts = torch.zeros((self.B, 2), dtype=torch.int32, device=d)
         _lib.check(self.lib.cit_cfr_target_count(_ptr(self.pool), self.B, self.node_cap, self.edge_cap, _ptr(roots),
                                                  int(mode), _ptr(counts), _stream()), "cit_cfr_target_count")
@@ -369,6 +373,22 @@ class GameBatch:
         _lib.check(self.lib.cit_cfr_arena_reset(_ptr(self.pool), self.B, node_cap, edge_cap, nb, eb, _stream()),
                    "cit_cfr_arena_reset")
 
+    def train_slice(self, iters, state, ticks, chosen, stats, running, flags=0):
+        """One cit_cfr_train_slice launch over the pool bound by _pool (state [B,16]
+        int32 CfrState, zero rows start a tree); `running` [1] int32 receives the
+        count of trees left unfinished."""
+        self._model_tree = False
+        _lib.check(self.lib.cit_cfr_train_slice(
+            _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx), _ptr(self.seer),
+            self.B, int(iters), int(flags), None, _ptr(self.pool), self.node_cap, self.edge_cap, _ptr(self.optbuf),
+            _ptr(state), int(ticks), _ptr(chosen), _ptr(stats), _ptr(running), _stream()), "cit_cfr_train_slice")
+
+    def release(self, lanes):
+        """Trees of `lanes` (device int32) give their arena blocks back (cit_cfr_arena_release)."""
+        lanes = lanes.to(device=self.device, dtype=torch.int32).contiguous()
+        _lib.check(self.lib.cit_cfr_arena_release(_ptr(self.pool), self.B, self.node_cap, self.edge_cap, _ptr(lanes),
+                                                  int(lanes.numel()), _stream()), "cit_cfr_arena_release")
+
     def arena_used(self):
         """(node blocks, edge blocks) handed out by the last search's arena and its
         capacity (node, edge); a count above capacity means it ran out."""
@@ -398,6 +418,7 @@ class GameBatch:
 
     def _cfr_pred(self, iters, net, max_depth, node_cap, edge_cap, max_rounds, flags=0, orig=None):
         self._pool(node_cap, edge_cap)
+        self._model_tree = True
         d = self.device
         o = self._orig(orig)
         state = torch.zeros((self.B, self.lib.cit_cfr_state_bytes() // 4), dtype=torch.int32, device=d)

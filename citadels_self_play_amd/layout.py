@@ -104,8 +104,14 @@ def cfr_node_block_bytes():
     return CFR_NB * (CFR_NODE_BYTES + GAME_BYTES)
 
 
+def cfr_ring_bytes(n_blocks, e_blocks):
+    """The arena's free-block rings (uint32 per block of each kind), padded to 16 B."""
+    return (4 * (n_blocks + e_blocks) + 15) // 16 * 16
+
+
 def cfr_arena_bytes(n_blocks, e_blocks):
-    return CFR_ARENA_HDR + n_blocks * cfr_node_block_bytes() + e_blocks * CFR_EB * CFR_EDGE_BYTES
+    return CFR_ARENA_HDR + cfr_ring_bytes(n_blocks, e_blocks) + n_blocks * cfr_node_block_bytes() + \
+        e_blocks * CFR_EB * CFR_EDGE_BYTES
 
 
 def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
@@ -117,8 +123,8 @@ def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
     nb, eb = cfr_nblocks(node_cap), cfr_eblocks(edge_cap)
     tbl = np.array(read(lane * per, 4 * (nb + eb))).view("<i4")
     hdr = np.array(read(B * per, 16)).view("<u4")
-    n_cap = int(hdr[1])
-    node_base = B * per + CFR_ARENA_HDR
+    n_cap, e_cap = int(hdr[1]), int(hdr[3])
+    node_base = B * per + CFR_ARENA_HDR + cfr_ring_bytes(n_cap, e_cap)
     row_base = node_base + n_cap * CFR_NB * CFR_NODE_BYTES
     edge_base = row_base + n_cap * CFR_NB * GAME_BYTES
 

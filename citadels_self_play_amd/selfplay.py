@@ -164,6 +164,132 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
     return b, torch.cat([p[0] for p in parts]), concat_targets([p[1] for p in parts], [p[0].shape[0] for p in parts])
 
 
+CP_DONE = 3                             # CfrState.phase of a finished tree (csrc/cit_cfr.h)
+
+
+def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_cap=None, device=None,
+                   slice_seconds=0.5, max_pool_bytes=None, arena_frac="auto", log=None):
+    """simulate_games through a tree queue: `slots` trees search at once (one
+    per workgroup, sharing one block arena); the search runs in slices of
+    ~slice_seconds (cit_cfr_train_slice), and after each slice the finished
+    trees' targets are extracted, their blocks released and their lanes given
+    the next positions, so a long tree no longer holds the whole batch.
+    Results (stats, targets in seed order, final games and streams) are those
+    of simulate_games bit for bit; trees that overflow are searched again
+    through GameBatch.cfr_decide (its retry).  Returns (batch of all seeds,
+    stats, targets)."""
+    from .engine import ERR_OVERFLOW, pool_bytes
+    if node_cap is None:
+        node_cap, ec = pool_caps(iters)
+        edge_cap = edge_cap or ec
+    edge_cap = edge_cap or 5 * node_cap
+    dev = torch.device(device or "cuda")
+    src = GameBatch(np.asarray(seeds, np.int64), preset=True, device=dev)
+    src.random_position(max_move)
+    src.seed_numpy()
+    term = src.terminal()
+    Q = src.B
+    snap = src._snapshot()
+    if max_pool_bytes is None:
+        torch.cuda.empty_cache()
+        max_pool_bytes = int(0.8 * torch.cuda.mem_get_info(dev)[0])
+    frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
+    S = min(Q, slots or Q)
+    while S > 1 and pool_bytes(S, node_cap, edge_cap, frac(S)) > max_pool_bytes:
+        S = max(1, min(S - 1, int(max_pool_bytes // (pool_bytes(S, node_cap, edge_cap, frac(S)) / S))))
+    sb = src.subset(torch.arange(S, device=dev))
+    sb.arena_frac = frac(S)
+    sb._pool(node_cap, edge_cap)
+    state = torch.zeros((S, 16), dtype=torch.int32, device=dev)
+    chosen = torch.zeros((S, 16), dtype=torch.uint8, device=dev)
+    stats = torch.zeros((S, 5), dtype=torch.int32, device=dev)
+    running = torch.zeros(1, dtype=torch.int32, device=dev)
+    out_stats = torch.zeros((Q, 5), dtype=torch.int32, device=dev)
+    slot_q = torch.arange(S, device=dev)         # queue index held by each slot (-1: idle)
+    parts, nxt, n_slices, n_done = [], S, 0, 0
+    ticks = max(1, int(slice_seconds * 1e8))
+    while True:
+        running.zero_()
+        sb.train_slice(iters, state, ticks, chosen, stats, running)
+        n_slices += 1
+        done = ((state[:, 6] == CP_DONE) & (slot_q >= 0)).nonzero().flatten()
+        if done.numel():
+            qs = slot_q[done]
+            out_stats[qs] = stats[done]
+            roots = torch.full((S,), -1, dtype=torch.int32, device=dev)
+            roots[done] = stats[done, 0]
+            parts.append((sb._cfr_targets(roots, 0), done, qs))
+            src.scatter(sb.subset(done), qs)
+            sb.release(done)
+            k = min(int(done.numel()), Q - nxt)
+            if k:
+                new_q = torch.arange(nxt, nxt + k, device=dev)
+                sb.scatter(src.subset(new_q), done[:k])
+                state[done[:k]] = 0
+                slot_q[done[:k]] = new_q
+                nxt += k
+            slot_q[done[k:]] = -1
+            n_done += int(done.numel())
+            if log is not None:
+                log("simulate_queue: %d of %d trees done after %d slices" % (n_done, Q, n_slices))
+        if int(running.item()) == 0 and bool((slot_q < 0).all()):
+            break
+    sb.pool = None
+    over = ((out_stats[:, 4] & ERR_OVERFLOW) != 0).nonzero().flatten()
+    if over.numel():                           # searched again with room to grow (cfr_decide's retry)
+        torch.cuda.empty_cache()
+        g, mt, idx, seer, npm, npi, steps = snap
+        sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),
+                                     seer[over].contiguous(), npm[:, over].contiguous(), npi[over].contiguous())
+        _, st2 = sub.cfr_decide(iters, node_cap, edge_cap)
+        out_stats[over] = st2
+        sub_roots = st2[:, 0].to(torch.int32)
+        extra = sub.cfr_targets(sub_roots, 0)
+        parts.append((extra, torch.arange(sub.B, device=dev), over))
+        src.scatter(sub, over)
+    t = _assemble_targets(parts, Q, exclude=over)
+    t["terminal"] = term
+    return src, out_stats, t
+
+
+def _assemble_targets(parts, n, exclude=None):
+    """cfr_targets dicts of trees spread over slot lanes -> one dict in output
+    lane order: part (t, slots, ids) holds output lanes `ids` in its lanes
+    `slots`; targets of `exclude` lanes are taken only from the last part."""
+    d = parts[0][0]["meta"].device
+    metas, firsts, feats, values, dists, opts = [], [], [], [], [], []
+    counts = torch.zeros((n, 2), dtype=torch.int32, device=d)
+    off = 0
+    for i, (t, slots, ids) in enumerate(parts):
+        m = torch.full((t["counts"].shape[0],), -1, dtype=torch.long, device=d)
+        m[slots] = ids.long()
+        if exclude is not None and exclude.numel() and i < len(parts) - 1:
+            m[slots[torch.isin(ids, exclude)]] = -1
+        meta = t["meta"].clone()
+        lane = m[meta[:, 0].long()]
+        keep = lane >= 0
+        meta[:, 0] = lane.to(meta.dtype)
+        metas.append(meta[keep])
+        firsts.append(t["meta"][:, 4].long()[keep] + off)
+        feats.append(t["feat"][keep])
+        values.append(t["value"][keep])
+        dists.append(t["dist"])
+        opts.append(t["opt_feat"])
+        off += t["dist"].shape[0]
+        ok = m[slots] >= 0
+        counts[ids[ok].long()] = t["counts"][slots[ok]]
+    meta = torch.cat(metas)
+    order = torch.sort(meta[:, 0].long() * (1 << 32) + torch.arange(meta.shape[0], device=d), stable=True).indices
+    meta = meta[order]
+    first = torch.cat(firsts)[order]
+    nch = meta[:, 3].long()
+    new_first = torch.cumsum(nch, 0) - nch
+    rows = torch.repeat_interleave(first - new_first, nch) + torch.arange(int(nch.sum()), device=d)
+    meta[:, 4] = new_first.to(meta.dtype)
+    return {"meta": meta, "feat": torch.cat(feats)[order], "value": torch.cat(values)[order],
+            "dist": torch.cat(dists)[rows], "opt_feat": torch.cat(opts)[rows], "counts": counts}
+
+
 def concat_targets(ts, sizes):
     """cfr_targets dicts of consecutive lane chunks -> one dict (lane and option
     row indices shifted)."""

@@ -143,7 +143,8 @@ int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1,
  * node_cap / edge_cap) followed by one arena (cit_cfr_arena_bytes(node_blocks,
  * edge_blocks)): a 64-byte header, node blocks (CFR_NB CfrNode records of
  * 168 B + CFR_NB packed game rows, 16-byte aligned) and edge blocks (CFR_EB
- * CfrEdge slots of 48 B).  A tree takes blocks as it grows, so the arena holds
+ * CfrEdge slots of 48 B), after a ring of free block ids per kind.  A
+ * tree takes blocks as it grows (a released block first), so the arena holds
  * what the trees use, not B worst cases; a tree that reaches its own caps or
  * finds the arena exhausted stops with CIT_ERR_OVERFLOW (search it again with
  * more room).  Opponent nodes reserve 10 edges, role-pick nodes 40 slots (10
@@ -194,6 +195,24 @@ int cit_skip_false_choice(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t*
 int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
                    int B, int iters, int flags, const int32_t* orig_player, void* pool, int node_cap, int edge_cap,
                    CitOption* optbuf, CitOption* chosen, int32_t* stats, hipStream_t stream);
+
+/* cit_cfr_decide in resumable slices (simulate_games' tree queue): each call
+ * advances every unfinished tree (state[l], B x cit_cfr_state_bytes(), zero
+ * before its first slice) for about slice_ticks of the 100 MHz GPU wall clock
+ * (0 = to the end), stopping at an iteration boundary; *running counts the
+ * trees that stopped unfinished.  A finished tree's chosen[l], stats[5*l..]
+ * and root game are written as cit_cfr_decide writes them; the tree, streams
+ * and counters are bit-identical to one cit_cfr_decide call.  With
+ * cit_cfr_arena_release a finished tree's lane can take the next tree (reset
+ * its state to zero) while the others run on. */
+int cit_cfr_train_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                        int B, int iters, int flags, const int32_t* orig_player, void* pool, int node_cap, int edge_cap,
+                        CitOption* optbuf, void* state, int64_t slice_ticks, CitOption* chosen, int32_t* stats,
+                        int32_t* running, hipStream_t stream);
+/* The blocks of trees lanes[0..n_lanes) (device array) back to the arena's
+ * free rings and their tables cleared; no search may run meanwhile. */
+int cit_cfr_arena_release(void* pool, int B, int node_cap, int edge_cap, const int32_t* lanes, int n_lanes,
+                          hipStream_t stream);
 
 /* Deep MCCFR with value-net leaves: cfr_pred(iters, max_depth)
  * (deep_mccfr.py:207-229) as run_mccfr runs it with a model and training=False
@@ -266,7 +285,11 @@ int cit_cfr_action_choice(void* pool, int B, int node_cap, int edge_cap, const i
  * mode 0: the whole tree (get_all_targets).  mode 1: the root only, no
  * threshold (run_utils.create_target_strategy + encode_options_from_node,
  * run_utils.py:89-109, as generate_test_data.py:18-26 uses them); feat may be
- * NULL (generate_test_data encodes the position before the search). */
+ * NULL (generate_test_data encodes the position before the search).  mode 2:
+ * mode 0 for trees searched without a model (cit_cfr_decide /
+ * cit_cfr_train_slice), whose visit counts only grow towards the root: the
+ * walk skips subtrees under the threshold (same output, a fraction of the
+ * nodes read). */
 int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
                          int32_t* counts, hipStream_t stream);
 int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode, uint32_t* mt,

@@ -82,7 +82,7 @@ class HostBatch:
 
 NODE_DT = np.dtype([("parent", "<i4"), ("first_edge", "<i4"), ("n_children", "<i2"), ("edge_cap", "<i2"),
                     ("depth", "<i2"), ("player", "i1"), ("gs_state", "i1"), ("flags", "u1"), ("winner", "i1"),
-                    ("pad", "u1", 6), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
+                    ("sib", "<i2"), ("pad", "u1", 4), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
 EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8"), ("S", "<f8"), ("CS", "<f8")])
 WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])
 assert NODE_DT.itemsize == 168 and EDGE_DT.itemsize == 48 and WIDE_DT.itemsize == 3 * 48
@@ -143,6 +143,20 @@ class HostCfr:
                               C.c_int(hb.B), C.c_int(iters), C.c_int(flags), _p(self.pool), C.c_int(self.node_cap),
                               C.c_int(self.edge_cap), _p(self.optbuf), _p(chosen), _p(stats))
         return chosen, stats
+
+    def train_slice(self, iters, state, slice_iters, chosen, stats, flags=0):
+        """One cit_cfr_train_slice call (budget: slice_iters iterations per tree);
+        returns the number of trees still running."""
+        hb = self.hb
+        return lib().cith_cfr_train_slice(_p(hb.games), _p(hb.mt), _p(hb.idx), _p(self.npmt), _p(self.npidx),
+                                          _p(hb.seer), C.c_int(hb.B), C.c_int(iters), C.c_int(flags), _p(self.pool),
+                                          C.c_int(self.node_cap), C.c_int(self.edge_cap), _p(self.optbuf), _p(state),
+                                          C.c_int(slice_iters), _p(chosen), _p(stats))
+
+    def release(self, lanes):
+        lanes = np.ascontiguousarray(lanes, np.int32)
+        lib().cith_cfr_arena_release(_p(self.pool), C.c_int(self.hb.B), C.c_int(self.node_cap), C.c_int(self.edge_cap),
+                                     _p(lanes), C.c_int(len(lanes)))
 
     def tree(self, l):
         nodes, edges, rows = L.cfr_tree_bytes(lambda o, n: self.pool[o:o + n], self.hb.B, l, self.node_cap,

@@ -1,0 +1,40 @@
+"""The tree queue on MI355X (selfplay.simulate_queue over cit_cfr_train_slice
++ cit_cfr_arena_release): 24 simulate_game trees through 5 lanes in slices of
+~20 µs .. 5 ms equal simulate_games' one launch bit for bit -- stats, targets
+in seed order, final games and both streams -- also when small node caps make
+trees overflow and go through the cfr_decide retry."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("meta", "feat", "value", "dist", "opt_feat", "counts", "terminal")
+
+
+def _same(a, b):
+    ba, sa, ta = a
+    bb, sb, tb = b
+    assert torch.equal(sa.cpu(), sb.cpu())
+    for k in KEYS:
+        assert torch.equal(ta[k].cpu(), tb[k].cpu()), k
+    for f in ("games", "mt", "mt_idx", "np_mt", "np_idx"):
+        assert torch.equal(getattr(ba, f).cpu(), getattr(bb, f).cpu()), f
+
+
+@pytest.mark.parametrize("slice_seconds", [2e-7, 5e-3])
+def test_gpu_queue_matches_batch(slice_seconds):
+    from citadels_self_play_amd import selfplay
+    seeds = selfplay.shard(24, 5150, 0, 1)
+    whole = selfplay.simulate_games(seeds, 2000)
+    q = selfplay.simulate_queue(seeds, 2000, slots=5, slice_seconds=slice_seconds)
+    _same(q, whole)
+    assert int((q[1][:, 4] != 0).sum()) == int((whole[1][:, 4] != 0).sum())
+
+
+def test_gpu_queue_overflow_retry():
+    from citadels_self_play_amd import selfplay
+    seeds = selfplay.shard(12, 6160, 0, 1)
+    whole = selfplay.simulate_games(seeds, 2000, node_cap=2048, edge_cap=8192)
+    q = selfplay.simulate_queue(seeds, 2000, slots=4, node_cap=2048, edge_cap=8192, slice_seconds=1e-3)
+    assert int(((whole[1][:, 1]) > 2048).sum()) > 0      # some trees outgrew the first caps
+    _same(q, whole)

@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--node-cap", type=int, default=None)
     ap.add_argument("--edge-cap", type=int, default=None, help="default engine.pool_caps(iters)")
+    ap.add_argument("--queue", type=int, default=0,
+                    help="config 5: this many trees per GPU through a tree queue of --batch lanes (selfplay.simulate_queue)")
+    ap.add_argument("--slice", type=float, default=0.5, help="queue slice seconds")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seed", type=int, default=30_000_000)
@@ -56,7 +59,8 @@ def main():
         net = models.ValueNet(m, dev)
     out = []
     for rep in range(a.warmup + a.reps):
-        seeds = selfplay.shard(B * world, base_seed=a.seed + rep * B * world)
+        n_per = a.queue if (a.config == 5 and a.queue) else B
+        seeds = selfplay.shard(n_per * world, base_seed=a.seed + rep * n_per * world)
         b = None
         if a.config in (3, 4):
             b = GameBatch(seeds, preset=True, device=dev)
@@ -73,8 +77,12 @@ def main():
         elif a.config == 4:
             chosen, stats, rounds = b.cfr_pred(iters, net, max_depth=10, node_cap=a.node_cap or 2048)
         else:
-            b, stats, t = selfplay.simulate_games(seeds, iters, node_cap=a.node_cap, edge_cap=a.edge_cap,
-                                                  log=(lambda m: print(m, file=sys.stderr, flush=True)))
+            logf = (lambda m: print(m, file=sys.stderr, flush=True))
+            if a.queue:
+                b, stats, t = selfplay.simulate_queue(seeds, iters, slots=B, node_cap=a.node_cap, edge_cap=a.edge_cap,
+                                                      slice_seconds=a.slice, log=logf)
+            else:
+                b, stats, t = selfplay.simulate_games(seeds, iters, node_cap=a.node_cap, edge_cap=a.edge_cap, log=logf)
             f, v = selfplay.all_gather_targets(t["feat"], t["value"])
             n_targets = int(f.shape[0])
             # k = 1 picks the final (terminal) game: ValueError in the reference
@@ -83,6 +91,8 @@ def main():
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        eb = stats[:, 4].to(dev)[~term.to(dev)]
+        err_bits = {hex(1 << k): int(((eb >> k) & 1).sum()) for k in range(12) if int(((eb >> k) & 1).sum())}
         st = stats.to(dev).to(torch.float64)
         tot = torch.tensor([el, float(st.shape[0]), float(st[:, 3].sum()), float(((st[:, 4] != 0) & ~term).sum()),
                             float(term.sum()), float(st[:, 1].sum()), float(st[:, 1].max()), float(st[:, 2].max())],
@@ -96,12 +106,13 @@ def main():
         el, units, carry, errs, terms, nodes, nodes_max, edges_max = [float(x) for x in tot]
         if rank == 0:
             print("rep %d: %.2fs" % (rep, el), file=sys.stderr, flush=True)
-        out.append({"config": a.config, "n_gpus": world, "per_gpu": B, "iters": iters, "seconds": el,
+        out.append({"config": a.config, "n_gpus": world, "per_gpu": int(units) // world, "lanes": B,
+                    "queue": bool(a.config == 5 and a.queue), "iters": iters, "seconds": el,
                     "warmup": rep < a.warmup,
                     ("trees_per_s" if a.config == 5 else "decisions_per_s"): units / el,
                     "carry_out_per_s": carry / el, "nodes_mean": nodes / units, "nodes_max": int(nodes_max), "edges_max": int(edges_max), "rounds": rounds,
                     "pooled_targets": n_targets, "error_lanes_nonterminal": int(errs),
-                    "terminal_positions": int(terms)})
+                    "terminal_positions": int(terms), "error_bits_rank0": err_bits})
     if rank == 0:
         timed = sorted([r for r in out if not r["warmup"]], key=lambda r: r["carry_out_per_s"])
         median = timed[len(timed) // 2] if timed else None

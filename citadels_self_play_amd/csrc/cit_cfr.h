@@ -899,6 +899,33 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
   CfrNode& N = cfr_node(T, n);
   CfrEdge* E = cfr_edge(T, N.first_edge);
   int nch = N.n_children;
+#if CIT_WAVE
+  if (nch <= 64) {
+    // lane a reads child a (one round of loads for all children); the max runs
+    // in the serial order over the lanes' values, so NaN / tie handling and
+    // every sum are the serial loop's
+    const int a = CFR_LANE;
+    if (!(N.flags & NF_ROLE_PICK)) {
+      int p = N.player;
+      double v = a < nch ? cfr_node(T, E[a].child).wp[p] : 0.0;
+      double mx = cfr_readlane_f64(v, 0);
+      for (int k = 1; k < nch; k++) {
+        double x = cfr_readlane_f64(v, k);
+        if (x > mx) mx = x;
+      }
+      if (a < nch) E[a].R += mx - v;
+    } else if (a < nch) {
+      CfrWide& W = cfr_wide(T, N.first_edge)[a];
+      const double* wp = cfr_node(T, E[a].child).wp;
+      double w[6];
+      for (int p = 0; p < 6; p++) w[p] = wp[p];
+      double mx = w[0];
+      for (int p = 1; p < 6; p++) mx = (mx != mx || w[p] != w[p]) ? NAN : (w[p] > mx ? w[p] : mx);
+      for (int p = 0; p < 6; p++) W.R[p] += mx - w[p];
+    }
+    return;
+  }
+#endif
   if (!(N.flags & NF_ROLE_PICK)) {
     int p = N.player;
     double mx = cfr_node(T, E[0].child).wp[p];

@@ -107,7 +107,7 @@ def arena_frac_for(B, node_cap):
 
 
 def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_cap=None, max_pool_bytes=None,
-                   log=None, arena_frac="auto"):
+                   log=None, arena_frac="auto", queue=True):
     """simulate_game (train_from_scratch.py:23-36, pretrain / training=True: the
     search ignores the model) for every seed: random.seed(s), np.random.seed(s),
     create_a_random_game(max_move), run_mccfr(iters, training=True),
@@ -119,9 +119,10 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
     summed worst case (default ARENA_FRAC: ~1.3x the measured mean; a tree
     that finds the arena exhausted is searched again, bit-identically, in a
     batch of its own).  When the seeds' pools do not fit in `max_pool_bytes`
-    (default: 80 % of the device memory not held by live tensors) the seeds
-    run in consecutive equal chunks and the results are concatenated in seed
-    order (the returned batch is then the last chunk's).
+    (default: 80 % of the device memory not held by live tensors) they go
+    through a tree queue over as many lanes as fit (simulate_queue; with
+    queue=False: consecutive equal chunks, the returned batch then being the
+    last chunk's); results are concatenated in seed order either way.
     targets["terminal"] [B] marks the positions that were already over (the
     reference's run_mccfr raises ValueError on them)."""
     from .engine import pool_bytes
@@ -139,6 +140,10 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
     while chunk > 1 and pool_bytes(chunk, node_cap, edge_cap, frac(chunk)) > max_pool_bytes:
         per = pool_bytes(chunk, node_cap, edge_cap, frac(chunk)) / chunk
         chunk = max(1, min(chunk - 1, int(max_pool_bytes // per)))
+    if chunk < len(seeds) and queue:
+        # more trees than fit at once: a tree queue over `chunk` lanes (same results)
+        return simulate_queue(seeds, iters, slots=chunk, max_move=max_move, node_cap=node_cap, edge_cap=edge_cap,
+                              device=dev, max_pool_bytes=max_pool_bytes, arena_frac=arena_frac, log=log)
     n_chunks = -(-len(seeds) // chunk)
     chunk = -(-len(seeds) // n_chunks)           # equal chunks: no short last launch
     parts = []

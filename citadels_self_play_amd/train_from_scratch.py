@@ -5,7 +5,8 @@ process per GPU:
 
 Each data round, every rank runs `--games-per-gpu` simulate_game trees
 (create_a_random_game(100) -> cfr_train(iters, training=True) ->
-get_all_targets) as one batch (selfplay.simulate_games); the (encode_game,
+get_all_targets) through selfplay.simulate_games (a tree queue over the
+~320 lanes whose pools fit in HBM); the (encode_game,
 node_value) pairs are pooled across ranks with an RCCL all-gather until
 `--min-targets` are collected (get_mccfr_targets, :45-63).  Rank 0 trains the
 value net (train.train_node_value_only) and the weights are broadcast.  The
@@ -54,8 +55,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200000)
     # 160 cfr_train(200000) pools (~1.3 GB each, engine.pool_caps) fill ~210 GB of
-    # the 288 GB HBM3E: one launch per round (simulate_games chunks if they do not fit)
-    ap.add_argument("--games-per-gpu", type=int, default=160)
+    # simulate_games runs as many 200k-iteration trees at once as the 288 GB HBM3E
+    # holds (~320) and queues the rest (selfplay.simulate_queue)
+    ap.add_argument("--games-per-gpu", type=int, default=960)
     ap.add_argument("--node-cap", type=int, default=None)
     ap.add_argument("--pretrain-targets", type=int, default=20000)
     ap.add_argument("--train-targets", type=int, default=5000)

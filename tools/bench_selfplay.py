@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--node-cap", type=int, default=None)
     ap.add_argument("--edge-cap", type=int, default=None, help="default engine.pool_caps(iters)")
-    ap.add_argument("--queue", type=int, default=0,
+    ap.add_argument("--queue", type=int, default=None,
                     help="config 5: this many trees per GPU through a tree queue of --batch lanes (selfplay.simulate_queue)")
     ap.add_argument("--slice", type=float, default=0.5, help="queue slice seconds")
     ap.add_argument("--reps", type=int, default=3)
@@ -46,11 +46,14 @@ def main():
     ap.add_argument("--seed", type=int, default=30_000_000)
     a = ap.parse_args()
     rank, world, dev = selfplay.init_distributed()
-    # config 5: 1024 trees per GPU at 20000 iterations (one wave per SIMD), 160 at
-    # the reference's 200000 (engine.pool_caps sizes the pools; ~1.3 GB per tree)
+    # config 5: 1024 trees per GPU at 20000 iterations (one wave per SIMD); 320 lanes
+    # at the reference's 200000 (block arenas hold ~0.5 of the worst case, ~0.7 GB
+    # per tree), fed 960 trees through the tree queue
     iters = a.iters or {3: 200, 4: 200, 5: 20000}[a.config]
+    if a.queue is None:      # config 5 at the reference's 200k: 3 trees per lane through the tree queue
+        a.queue = 960 if (a.config == 5 and iters > 20000 and not a.batch) else 0
     B = a.batch or {3: 1024, 4: 4096 // max(1, world) if world > 1 else 4096,
-                    5: 1024 if iters <= 20000 else 160}[a.config]
+                    5: 1024 if iters <= 20000 else 320}[a.config]
     net = None
     if a.config == 4:
         from citadels_self_play_amd import models

@@ -56,7 +56,7 @@ def build():
 
 def _workload(GameBatch, pool_caps, torch, B, iters):
     b = GameBatch(np.arange(20_000_000, 20_000_000 + B), preset=True)
-    if iters == 200:
+    if iters <= 200:
         b.advance_random(0, 300)
     else:
         b.random_position(100)
@@ -72,7 +72,7 @@ def _workload(GameBatch, pool_caps, torch, B, iters):
     return t0.elapsed_time(t1), stats.cpu().numpy()
 
 
-def run(which=None):
+def run(which=None, workloads=None):
     import torch
     import citadels_self_play_amd._lib as LL
     from citadels_self_play_amd.engine import GameBatch, pool_caps
@@ -85,7 +85,9 @@ def run(which=None):
         if vname != "plain":
             lib.cit_prof_read.argtypes = [C.c_void_p]
             buf = (C.c_ulonglong * 64)()
-        for tag, B, iters in (("config3", 1024, 200), ("config5_2000", 1024, 2000)):
+        wl = (("config3", 1024, 200), ("config5_2000", 1024, 2000)) if not workloads else \
+            [("iters%s_b%s" % tuple(w.split(":")), int(w.split(":")[1]), int(w.split(":")[0])) for w in workloads.split(",")]
+        for tag, B, iters in wl:
             if vname != "plain":
                 lib.cit_prof_read(buf)
             ms, st = _workload(GameBatch, pool_caps, torch, B, iters)
@@ -105,4 +107,4 @@ def run(which=None):
 
 
 if __name__ == "__main__":
-    build() if sys.argv[1:] == ["build"] else run(*sys.argv[2:])
+    build() if sys.argv[1:] == ["build"] else run(*sys.argv[2:])   # run [variant] [iters:B,...]

@@ -29,12 +29,13 @@ def test_gpu_shard_invariance_simulate_games():
     t = selfplay.concat_targets([p[2] for p in parts], [p[1].shape[0] for p in parts])
     for k in ("meta", "feat", "value", "dist", "opt_feat", "counts"):
         assert torch.equal(t[k].cpu(), whole_t[k].cpu()), k
-    # and in memory-bounded chunks (3 trees per chunk) within one rank
-    cb, cstats, ct = selfplay.simulate_games(selfplay.shard(n, 4242, 0, 1), iters,
-                                             max_pool_bytes=pool_bytes(3, whole_b.node_cap, whole_b.edge_cap))
-    assert torch.equal(cstats.cpu(), whole_stats.cpu())
-    for k in ("meta", "feat", "value", "dist", "opt_feat", "counts"):
-        assert torch.equal(ct[k].cpu(), whole_t[k].cpu()), k
+    # and memory-bounded (3 trees at a time) within one rank: chunks, and the tree queue
+    for queue in (False, True):
+        cb, cstats, ct = selfplay.simulate_games(selfplay.shard(n, 4242, 0, 1), iters, queue=queue,
+                                                 max_pool_bytes=pool_bytes(3, whole_b.node_cap, whole_b.edge_cap))
+        assert torch.equal(cstats.cpu(), whole_stats.cpu())
+        for k in ("meta", "feat", "value", "dist", "opt_feat", "counts"):
+            assert torch.equal(ct[k].cpu(), whole_t[k].cpu()), k
 
 
 def _port():

@@ -4,6 +4,7 @@ build of the engine headers, against the reference's outputs
 (tests/golden/targets2000.json.gz): positions, trees, decisions, RNG end
 states and every target tuple (regret targets rtol 1e-12, np.exp)."""
 import numpy as np
+import pytest
 
 from citadels_self_play_amd import canon
 from citadels_self_play_amd import layout as L
@@ -13,7 +14,8 @@ from test_cfr_host_golden import hash_obj
 from test_targets_oracle_golden import check_targets
 
 
-def test_host_targets_match_reference():
+@pytest.mark.parametrize("mode", [0, 2])      # 2: the pruned walk (trees searched without a model)
+def test_host_targets_match_reference(mode):
     recs = load_golden("targets2000.json.gz")
     hb = HostBatch([r["seed"] for r in recs], True)
     random_position(hb, 100)
@@ -21,7 +23,7 @@ def test_host_targets_match_reference():
         assert canon.canon_game(hb.game(l)) == r["position"], r["seed"]
     cf = HostCfr(hb, node_cap=8192, edge_cap=8 * 8192)
     chosen, stats = cf.decide(2000)
-    t = cfr_targets(cf, stats[:, 0])
+    t = cfr_targets(cf, stats[:, 0], mode=mode)
     per = split_targets(t)
     for l, r in enumerate(recs):
         root, n_nodes, n_edges, carry, err = stats[l]

@@ -2,7 +2,8 @@
 + cit_cfr_arena_release): 24 simulate_game trees through 5 lanes in slices of
 ~20 µs .. 5 ms equal simulate_games' one launch bit for bit -- stats, targets
 in seed order, final games and both streams -- also when small node caps make
-trees overflow and go through the cfr_decide retry."""
+trees overflow or the shared arena runs out and trees go through the
+cfr_decide retry."""
 import pytest
 import torch
 
@@ -37,4 +38,14 @@ def test_gpu_queue_overflow_retry():
     whole = selfplay.simulate_games(seeds, 2000, node_cap=2048, edge_cap=8192)
     q = selfplay.simulate_queue(seeds, 2000, slots=4, node_cap=2048, edge_cap=8192, slice_seconds=1e-3)
     assert int(((whole[1][:, 1]) > 2048).sum()) > 0      # some trees outgrew the first caps
+    _same(q, whole)
+
+
+def test_gpu_queue_arena_exhausted():
+    # an arena far below the trees' needs: trees that find it exhausted stop
+    # with the overflow bit and are searched again (cfr_decide), same results
+    from citadels_self_play_amd import selfplay
+    seeds = selfplay.shard(10, 7170, 0, 1)
+    whole = selfplay.simulate_games(seeds, 2000)
+    q = selfplay.simulate_queue(seeds, 2000, slots=6, arena_frac=(0.05, 0.05), slice_seconds=1e-3)
     _same(q, whole)

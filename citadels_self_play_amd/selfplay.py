@@ -99,6 +99,8 @@ def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None):
 # trees average ~1.35 nodes / iteration against pool_caps' 3.5.
 ARENA_FRAC = (0.5, 0.8)
 ARENA_MIN_TREES, ARENA_MIN_BLOCKS = 32, 16
+# Tree-queue slots per slot that fits at ARENA_FRAC (simulate_queue's overcommit).
+QUEUE_OVERCOMMIT = 2.0
 
 
 def arena_frac_for(B, node_cap):
@@ -172,18 +174,90 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
 CP_DONE = 3                             # CfrState.phase of a finished tree (csrc/cit_cfr.h)
 
 
+class _SlicePlanner:
+    """Which trees of an overcommitted tree queue search in the next slice.
+
+    With more slots than the arena holds at the trees' final sizes, the queue
+    relies on trees being at different stages of growth (a tree holds, on
+    average over its life, about half its final blocks).  Before each slice
+    the planner reads every tree's held blocks (its block tables) and its
+    iteration count, and lets trees run, most advanced first, while the
+    arena's free blocks cover their expected growth over one slice (the
+    growth each showed in its last slice, else the largest growth seen) with
+    `margin`; the rest sit the slice out (paused: CfrState.phase reads
+    CP_DONE for one launch, so the kernel returns at once).  Trees enter
+    paused and start when the arena has room: the queue staggers itself, and
+    the most advanced trees, which release the most blocks when they finish,
+    always go first.  The oldest tree always runs; if the arena still runs
+    out it overflows and is searched again after the queue (simulate_queue's
+    retry), so pausing never changes a result, only where the search waits."""
+
+    def __init__(self, sb, node_cap, edge_cap, margin=1.5):
+        from . import layout as L
+        self.nbt, self.ebt = L.cfr_nblocks(node_cap), L.cfr_eblocks(edge_cap)
+        per = L.cfr_pool_bytes(node_cap, edge_cap) // 4
+        self.tables = sb.pool[:sb.B * per * 4].view(torch.int32).view(sb.B, per)[:, :self.nbt + self.ebt]
+        self.cap = np.array(sb.arena, np.int64)
+        self.margin = margin
+        self.last_held = np.zeros((sb.B, 2), np.int64)
+        self.growth = np.full((sb.B, 2), -1, np.int64)      # blocks per slice (-1: not seen running)
+        self.prior = np.array([max(2, self.nbt // 16), max(2, self.ebt // 16)], np.int64)
+        self.paused_slices = 0
+
+    def held(self):
+        t = (self.tables >= 0)
+        return torch.stack([t[:, :self.nbt].sum(1), t[:, self.nbt:].sum(1)], 1).cpu().numpy().astype(np.int64)
+
+    def plan(self, state_np, live, ran):
+        """live: slots holding an unfinished tree; ran: slots that searched in the
+        last slice.  Returns the bool mask of live slots to pause."""
+        held = self.held()
+        grew = held - self.last_held
+        seen = ran & (grew.sum(1) > 0)
+        self.growth[seen] = grew[seen]
+        if seen.any():
+            self.prior = np.maximum(self.prior, grew[seen].max(0))
+        self.last_held = held
+        free = self.cap - held.sum(0)
+        order = np.flatnonzero(live)
+        order = order[np.argsort(-state_np[order, 5], kind="stable")]       # most iterations first
+        pause = np.zeros(live.shape[0], bool)
+        for k, i in enumerate(order):
+            g = self.growth[i] if self.growth[i, 0] >= 0 else self.prior
+            need = np.ceil(g * self.margin).astype(np.int64) + 1
+            if k == 0 or (need <= free).all():
+                free -= need
+            else:
+                pause[i] = True
+        self.paused_slices += int(pause.sum())
+        return pause
+
+    def reset(self, slots):
+        """`slots` (numpy indices) took new trees."""
+        self.growth[slots] = -1
+        self.last_held[slots] = 0
+
+
 def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_cap=None, device=None,
-                   slice_seconds=0.5, max_pool_bytes=None, arena_frac="auto", log=None):
+                   slice_seconds=0.5, max_pool_bytes=None, arena_frac="auto", log=None, overcommit=None):
     """simulate_games through a tree queue: `slots` trees search at once (one
     per workgroup, sharing one block arena); the search runs in slices of
     ~slice_seconds (cit_cfr_train_slice), and after each slice the finished
     trees' targets are extracted, their blocks released and their lanes given
     the next positions, so a long tree no longer holds the whole batch.
+
+    overcommit > 1 (default QUEUE_OVERCOMMIT for large trees): the arena
+    takes all of max_pool_bytes and the queue runs `overcommit` times the
+    slots that fit at ARENA_FRAC, relying on trees being at different stages
+    of growth; _SlicePlanner pauses the least advanced trees for a slice when
+    the arena's free blocks do not cover everyone's growth.
+
     Results (stats, targets in seed order, final games and streams) are those
     of simulate_games bit for bit; trees that overflow are searched again
     through GameBatch.cfr_decide (its retry).  Returns (batch of all seeds,
     stats, targets)."""
     from .engine import ERR_OVERFLOW, pool_bytes
+    from . import layout as L
     if node_cap is None:
         node_cap, ec = pool_caps(iters)
         edge_cap = edge_cap or ec
@@ -202,9 +276,24 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     S = min(Q, slots or Q)
     while S > 1 and pool_bytes(S, node_cap, edge_cap, frac(S)) > max_pool_bytes:
         S = max(1, min(S - 1, int(max_pool_bytes // (pool_bytes(S, node_cap, edge_cap, frac(S)) / S))))
+    if overcommit is None:
+        overcommit = QUEUE_OVERCOMMIT if (arena_frac == "auto" and frac(S) is not None) else 1.0
+    arena_f = frac(S)
+    if overcommit > 1 and arena_f is not None and S < Q:
+        # the same bytes as S trees at ARENA_FRAC, shared by more slots
+        fn, fe = arena_f if isinstance(arena_f, tuple) else (arena_f, arena_f)
+        nbt, ebt = L.cfr_nblocks(node_cap), L.cfr_eblocks(edge_cap)
+        nb0, eb0 = fn * S * nbt, fe * S * ebt
+        S2 = min(Q, int(S * overcommit))
+        scale = (max_pool_bytes - S2 * L.cfr_pool_bytes(node_cap, edge_cap)) / float(
+            L.cfr_arena_bytes(int(nb0), int(eb0)))
+        S, arena_f = S2, (min(1.0, nb0 * scale / (S2 * nbt)), min(1.0, eb0 * scale / (S2 * ebt)))
+    else:
+        overcommit = 1.0
     sb = src.subset(torch.arange(S, device=dev))
-    sb.arena_frac = frac(S)
+    sb.arena_frac = arena_f
     sb._pool(node_cap, edge_cap)
+    planner = _SlicePlanner(sb, node_cap, edge_cap) if overcommit > 1 else None
     state = torch.zeros((S, 16), dtype=torch.int32, device=dev)
     chosen = torch.zeros((S, 16), dtype=torch.uint8, device=dev)
     stats = torch.zeros((S, 5), dtype=torch.int32, device=dev)
@@ -213,10 +302,24 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     slot_q = torch.arange(S, device=dev)         # queue index held by each slot (-1: idle)
     parts, nxt, n_slices, n_done = [], S, 0, 0
     ticks = max(1, int(slice_seconds * 1e8))
+    ran = np.zeros(S, bool)
     while True:
         running.zero_()
+        paused = None
+        if planner is not None:
+            st_np = state.cpu().numpy()
+            live = (slot_q.cpu().numpy() >= 0) & (st_np[:, 6] != CP_DONE)
+            pmask = planner.plan(st_np, live, ran)
+            ran = live & ~pmask
+            if pmask.any():
+                paused = torch.from_numpy(np.flatnonzero(pmask)).to(dev)
+                saved = state[paused, 6].clone()
+                state[paused, 6] = CP_DONE           # sits this slice out (the kernel returns at once)
         sb.train_slice(iters, state, ticks, chosen, stats, running)
         n_slices += 1
+        if paused is not None:
+            state[paused, 6] = saved
+            running += int(paused.numel())         # paused trees are unfinished
         done = ((state[:, 6] == CP_DONE) & (slot_q >= 0)).nonzero().flatten()
         if done.numel():
             qs = slot_q[done]
@@ -231,6 +334,8 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
                 new_q = torch.arange(nxt, nxt + k, device=dev)
                 sb.scatter(src.subset(new_q), done[:k])
                 state[done[:k]] = 0
+                if planner is not None:
+                    planner.reset(done[:k].cpu().numpy())
                 slot_q[done[:k]] = new_q
                 nxt += k
             slot_q[done[k:]] = -1
@@ -239,6 +344,8 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
                 log("simulate_queue: %d of %d trees done after %d slices" % (n_done, Q, n_slices))
         if int(running.item()) == 0 and bool((slot_q < 0).all()):
             break
+    if log is not None and planner is not None:
+        log("simulate_queue: %d slots (overcommit %.2f), %d tree-slices paused" % (S, overcommit, planner.paused_slices))
     sb.pool = None
     over = ((out_stats[:, 4] & ERR_OVERFLOW) != 0).nonzero().flatten()
     if over.numel():                           # searched again with room to grow (cfr_decide's retry)

@@ -49,3 +49,18 @@ def test_gpu_queue_arena_exhausted():
     whole = selfplay.simulate_games(seeds, 2000)
     q = selfplay.simulate_queue(seeds, 2000, slots=6, arena_frac=(0.05, 0.05), slice_seconds=1e-3)
     _same(q, whole)
+
+
+@pytest.mark.parametrize("overcommit,frac", [(3.0, (1.0, 1.0)), (2.5, (0.3, 0.5))])
+def test_gpu_queue_overcommit_pauses(overcommit, frac):
+    # more slots than the arena holds at the trees' final sizes: the slice
+    # planner pauses the least advanced trees (and, with the tiny arena, trees
+    # still overflow and go through the retry); results are unchanged
+    from citadels_self_play_amd import selfplay
+    seeds = selfplay.shard(20, 8180, 0, 1)
+    whole = selfplay.simulate_games(seeds, 2000)
+    msgs = []
+    q = selfplay.simulate_queue(seeds, 2000, slots=4, arena_frac=frac, overcommit=overcommit, slice_seconds=2e-3,
+                                log=msgs.append)
+    _same(q, whole)
+    assert any("tree-slices paused" in m for m in msgs)

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--queue", type=int, default=None,
                     help="config 5: this many trees per GPU through a tree queue of --batch lanes (selfplay.simulate_queue)")
     ap.add_argument("--slice", type=float, default=0.5, help="queue slice seconds")
+    ap.add_argument("--overcommit", type=float, default=None,
+                    help="queue slots per slot that fits at ARENA_FRAC (default selfplay.QUEUE_OVERCOMMIT)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seed", type=int, default=30_000_000)
@@ -83,7 +85,7 @@ def main():
             logf = (lambda m: print(m, file=sys.stderr, flush=True))
             if a.queue:
                 b, stats, t = selfplay.simulate_queue(seeds, iters, slots=B, node_cap=a.node_cap, edge_cap=a.edge_cap,
-                                                      slice_seconds=a.slice, log=logf)
+                                                      slice_seconds=a.slice, log=logf, overcommit=a.overcommit)
             else:
                 b, stats, t = selfplay.simulate_games(seeds, iters, node_cap=a.node_cap, edge_cap=a.edge_cap, log=logf)
             f, v = selfplay.all_gather_targets(t["feat"], t["value"])
@@ -110,6 +112,8 @@ def main():
         if rank == 0:
             print("rep %d: %.2fs" % (rep, el), file=sys.stderr, flush=True)
         out.append({"config": a.config, "n_gpus": world, "per_gpu": int(units) // world, "lanes": B,
+                    "overcommit": a.overcommit if a.overcommit is not None else
+                    (selfplay.QUEUE_OVERCOMMIT if (a.config == 5 and a.queue) else None),
                     "queue": bool(a.config == 5 and a.queue), "iters": iters, "seconds": el,
                     "warmup": rep < a.warmup,
                     ("trees_per_s" if a.config == 5 else "decisions_per_s"): units / el,

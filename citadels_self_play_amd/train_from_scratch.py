@@ -5,8 +5,9 @@ process per GPU:
 
 Each data round, every rank runs `--games-per-gpu` simulate_game trees
 (create_a_random_game(100) -> cfr_train(iters, training=True) ->
-get_all_targets) through selfplay.simulate_games (a tree queue over the
-~320 lanes whose pools fit in HBM); the (encode_game,
+get_all_targets) through selfplay.simulate_games (a tree queue over ~640
+slots sharing a block arena of ~0.8 of HBM, the least advanced trees paused
+for a slice when it runs short); the (encode_game,
 node_value) pairs are pooled across ranks with an RCCL all-gather until
 `--min-targets` are collected (get_mccfr_targets, :45-63).  Rank 0 trains the
 value net (train.train_node_value_only) and the weights are broadcast.  The

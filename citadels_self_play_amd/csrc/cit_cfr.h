@@ -356,6 +356,17 @@ CIT_NOINLINE CfrCnt eng_list_lds(CfrTree& T_in, int which) {
   cit_enum_options(cfr_w(T, cfr_u(which)), s, cfr_glb(T.seer));
   return {s.n, s.err};
 }
+// skip_false_choice's question (exactly one option?): the options of working
+// row `which` into the LDS list buffer until a second one is known (n is then
+// a lower bound >= 2), unless the enumeration may still raise (Upto2Sink).
+CIT_NOINLINE CfrCnt eng_list_upto2(CfrTree& T_in, int which) {
+  CIT_PROF_SCOPE(2);
+  CfrTree& T = CFR_T(T_in);
+  const CitGame& g = cfr_w(T, cfr_u(which));
+  Upto2Sink s(cfr_lbuf(T), CFR_LBUF, cfr_u(cit_enum_late_error(g) ? 0 : 1) != 0);
+  cit_enum_options(g, s, cfr_glb(T.seer));
+  return {s.n, s.err};
+}
 CIT_NOINLINE void eng_sample(CfrTree& T_in, int which, int orig, int role_sample) {
   CIT_PROF_SCOPE(5);
   CfrTree& T = CFR_T(T_in);
@@ -578,7 +589,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   int n = 0;
   if (!cfr_u(skipped)) {
     eng_prepare(T, which);
-    CfrCnt c = cfr_ucnt(eng_list_lds(T, which));
+    CfrCnt c = cfr_ucnt(eng_list_upto2(T, which));
     n = c.n;
     e |= c.err;
   }
@@ -590,7 +601,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
     int win = cfr_u(eng_carry(T, which, o));
     done = win >= 0;
     eng_prepare(T, which);
-    CfrCnt c = cfr_ucnt(eng_list_lds(T, which));
+    CfrCnt c = cfr_ucnt(eng_list_upto2(T, which));
     n = c.n;
     e |= c.err;
     if (i > 100) done = true;

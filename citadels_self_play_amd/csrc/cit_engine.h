@@ -847,6 +847,41 @@ struct BufSink {
   CIT_WAVE_LIST_EMIT
 };
 
+// skip_false_choice only asks whether a state has exactly one option: this
+// sink lists like ListSink but, when `stop` is set, ends the enumeration once
+// a second option is known (n is then a lower bound >= 2).  Callers clear
+// `stop` where the full enumeration may still raise after emitting options
+// (cit_enum_late_error), so the error bits are the full enumeration's.
+struct Upto2Sink {
+  CitOpt* buf;
+  int cap;
+  int n = 0;
+  uint32_t err = 0;
+  bool stop;
+  CIT_HD Upto2Sink(CitOpt* b, int c, bool s) : buf(b), cap(c), stop(s) {}
+  CIT_HD bool emit(const CitOpt& o) {
+    if (n < cap) buf[n] = o;
+    n++;
+    return stop && n >= 2;
+  }
+  template <class F> CIT_HD bool block(int cnt, F&& f) {
+    int m = cap - n < cnt ? cap - n : cnt;
+    if (stop && m > 2) m = 2;
+    for (int i = 0; i < m; i++) buf[n + i] = f(i);
+    n += cnt;
+    return stop && n >= 2;
+  }
+#if CIT_WAVE
+  CIT_HD bool wave_emit(bool p, const CitOpt& o) {
+    uint64_t m = cit_ballot(p);
+    int r = n + cit_lane_rank(m);
+    if (p && r < cap) buf[r] = o;
+    n += __popcll(m);
+    return stop && n >= 2;
+  }
+#endif
+};
+
 #define EMIT(...)                                  \
   do {                                             \
     if (s.emit(__VA_ARGS__)) return true;          \
@@ -1430,6 +1465,15 @@ CIT_HD void cit_prepare_options(CitGame& g, CitMT& rng, uint64_t* seer) {
     g.sch[g.n_sch++] = (uint8_t)c;
     i++;
   }
+}
+
+// Whether the enumeration of g may raise after it has emitted options: only
+// the blackmailer's character options raise late (gen_role: a possessed rank
+// outside 2..7 after the build options were listed); every other error of
+// cit_enum_options comes before the first option of its branch.
+CIT_HD bool cit_enum_late_error(const CitGame& g) {
+  int a = g.gs_pid;
+  return a >= 0 && a < CIT_NP && g.pl[a].role == R_BLACKMAILER;
 }
 
 CIT_HD int cit_count_options(const CitGame& g, uint32_t& err, const uint64_t* seer) {

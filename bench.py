@@ -217,6 +217,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="games per GPU")
     ap.add_argument("--games-per-block", type=int, default=0, help="0 = k_rollout_u (one game per workgroup)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams the K timed batches are launched round-robin on (1 = one after another)")
     ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per C++ CPU-baseline leg")
     ap.add_argument("--py-seconds", type=float, default=2.0, help="Python-oracle CPU figure")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -248,14 +250,15 @@ def main():
     from citadels_self_play_amd import layout as L
     from citadels_self_play_amd.engine import GameBatch
 
-    B, K, W = args.batch, args.steps, args.warmup
+    B, K, W, S = args.batch, args.steps, args.warmup, max(1, args.streams)
     seer = None
     batches = []
     for step in range(W + K):
         s0 = BASE_SEED + (step * world + rank) * B
         gb = GameBatch(np.arange(s0, s0 + B), preset=True, device=dev, games_per_block=args.games_per_block,
                        seer=seer)
-        seer = gb.seer
+        if S == 1:          # the seer scratch is per lane: batches in flight together need their own
+            seer = gb.seer
         batches.append(gb)
     torch.cuda.synchronize()
 
@@ -263,17 +266,22 @@ def main():
         gb.rollout()
     torch.cuda.synchronize()
 
-    # HIP events on the stream the kernel is launched on (torch's current stream)
+    # HIP events on the stream each kernel is launched on.  With S > 1 streams
+    # batch k goes to stream k % S, so the next batches' games take the SIMD
+    # slots the finished games of earlier batches leave (the launch tail).
     stream = torch.cuda.current_stream()
+    streams = [stream] if S == 1 else [torch.cuda.Stream(device=dev) for _ in range(S)]
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k, gb in enumerate(batches[W:]):
-        evs[k][0].record(stream)
-        gb.rollout()
-        evs[k][1].record(stream)
+        st = streams[k % S]
+        with torch.cuda.stream(st):
+            evs[k][0].record(st)
+            gb.rollout()
+            evs[k][1].record(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -281,6 +289,27 @@ def main():
 
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     trans_rank = sum(int(gb.steps.sum().item()) for gb in batches[W:])
+    serial = None
+    if S > 1:
+        # The roofline prices one launch running alone: replay the same K
+        # batches one after another on one stream (re-initialised, untimed init).
+        for gb in batches[W:]:
+            gb.reset()
+        torch.cuda.synchronize()
+        sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        ts = time.perf_counter()
+        for k, gb in enumerate(batches[W:]):
+            sev[k][0].record(stream)
+            gb.rollout()
+            sev[k][1].record(stream)
+        torch.cuda.synchronize()
+        el_s = time.perf_counter() - ts
+        trans_s = sum(int(gb.steps.sum().item()) for gb in batches[W:])
+        overlapped_ms = float(np.mean(kernel_ms))
+        kernel_ms = [a.elapsed_time(b) for a, b in sev]
+        serial = {"value_rank0": trans_s / el_s, "ms_per_step": el_s / K * 1e3,
+                  "same_transitions": trans_s == trans_rank,
+                  "overlapped_launch_avg_ms": overlapped_ms}
     # the launch lasts as long as its longest game (one wave per game, latency-bound)
     steps_max = float(np.mean([int(gb.steps.max().item()) for gb in batches[W:]]))
     errs = sum(int((gb.errors() != 0).sum().item()) for gb in batches[W:])
@@ -353,6 +382,9 @@ def main():
                                      "us_per_step_longest_game": avg_ms * 1e3 / steps_max,
                                      "mean_over_max": per_launch_trans / B / steps_max},
                          "pmc": pmc},
+            "streams": {"n": S, "one_stream": serial,
+                        "note": "K batches launched round-robin on n HIP streams (n = 1: one after another); "
+                                "roofline from one launch running alone"},
             "e2e": {"games_per_s": world * B * K / elapsed_e2e, "transitions_per_s": trans_all / elapsed_e2e,
                     "init_ms_per_batch": init_ms,
                     "note": "k_init (CPython init_by_array seeding + preset deal) inside the timed region"},

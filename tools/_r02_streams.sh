@@ -1,0 +1,13 @@
+#!/bin/bash
+# bench.py --streams A/B: 1 / 2 / 4 / 8 streams interleaved, 3 reps, default K/W.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/streams
+mkdir -p $O
+for r in 1 2 3; do
+  for s in 1 2 4 8; do
+    timeout -k 10 120 python bench.py --streams $s --no-pmc --no-cpu-baseline >> $O/s$s.jsonl 2>> $O/err.log || exit 1
+    echo "rep $r streams $s done"
+  done
+done
+timeout -k 10 120 python bench.py --streams 4 --steps 20 --no-pmc --no-cpu-baseline >> $O/s4_k20.jsonl 2>> $O/err.log

@@ -7,12 +7,18 @@ to terminal.  One bench step = one launch of the fused rollout kernel
 (initialised, untimed, before the timed region); seeds are disjoint across
 steps and ranks (seed = base + (step * world + rank) * B + lane), so N GPUs
 play N x 4096 independent games per step (weak scaling, no data-path
-collective).
+collective).  The K steps are launched round-robin on `--streams` HIP
+streams (default 2, warmed before the timed region): a launch lasts as long
+as its longest game, and the next batch's games take the SIMD slots the
+finished games free (tests/test_gpu_parity.py::test_gpu_rollout_streams_overlap
+checks overlapped batches equal batches run alone).  `streams.one_stream`
+replays the same K batches one after another for comparison.
 
 Prints ONE JSON line on rank 0.  `value` = carry_out transitions of all ranks
 / max-over-ranks wall time of the K timed steps.
 
-* `roofline` prices k_rollout_u by its algorithmic bytes (2 x CIT_GAME_BYTES
+* `roofline` prices one k_rollout_u launch running alone (the one-stream
+  replay; the PMC children run with --streams 1) by its algorithmic bytes (2 x CIT_GAME_BYTES
   per transition) over its HIP-event duration against HBM
   peak; `traffic` is the HBM bytes per launch measured IN THIS RUN by two
   rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child run of
@@ -154,7 +160,8 @@ def _pmc_pass(counters, outdir, timeout_s=150):
     os.makedirs(outdir, exist_ok=True)
     cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", outdir, "-o", "run", "--",
                                               sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2",
-                                              "--warmup", "1", "--no-cpu-baseline", "--no-pmc"]
+                                              "--warmup", "1", "--streams", "1", "--no-cpu-baseline",
+                                              "--no-pmc"]
     env = dict(os.environ, TMPDIR="/tmp")
     with open(os.path.join(outdir, "log.txt"), "w") as log:
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
@@ -217,7 +224,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="games per GPU")
     ap.add_argument("--games-per-block", type=int, default=0, help="0 = k_rollout_u (one game per workgroup)")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the K timed batches are launched round-robin on (1 = one after another)")
     ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per C++ CPU-baseline leg")
     ap.add_argument("--py-seconds", type=float, default=2.0, help="Python-oracle CPU figure")
@@ -271,6 +278,15 @@ def main():
     # slots the finished games of earlier batches leave (the launch tail).
     stream = torch.cuda.current_stream()
     streams = [stream] if S == 1 else [torch.cuda.Stream(device=dev) for _ in range(S)]
+    if S > 1:
+        # A stream's first launches set up its hardware queue: warm every stream
+        # with a small rollout of its own (untimed, seeds outside the timed ones).
+        for i, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                for _ in range(2):
+                    GameBatch(np.arange(BASE_SEED - (i + 1) * 256, BASE_SEED - i * 256), preset=True, device=dev,
+                              games_per_block=args.games_per_block).rollout()
+        torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if world > 1:
         dist.barrier()

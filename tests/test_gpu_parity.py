@@ -170,6 +170,32 @@ def test_gpu_full_size_properties(engine):
         assert canon.canon_game(L.game_from_bytes(rows_a[l])) == O.canon(og), l
 
 
+def test_gpu_rollout_streams_overlap(engine):
+    """bench.py --streams: 8 batches of 4096 games launched round-robin on 4
+    HIP streams (k_rollout_u launches overlapping) give the same rows, steps
+    and winners as each batch rolled out alone on one stream."""
+    B, K, S = 4096, 8, 4
+    seeds = [np.arange(8_000_000 + k * B, 8_000_000 + (k + 1) * B) for k in range(K)]
+    alone = []
+    for s in seeds:
+        a = engine(s, preset=True)
+        st, w = a.rollout(games_per_block=0)
+        torch.cuda.synchronize()
+        alone.append((a.rows(), st.cpu().numpy().copy(), w.cpu().numpy().copy()))
+    batches = [engine(s, preset=True) for s in seeds]
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    torch.cuda.synchronize()
+    for k, gb in enumerate(batches):
+        with torch.cuda.stream(streams[k % S]):
+            gb.rollout(games_per_block=0)
+    torch.cuda.synchronize()
+    for k, gb in enumerate(batches):
+        assert int((gb.errors() != 0).sum()) == 0, k
+        assert np.array_equal(gb.rows(), alone[k][0]), k
+        assert np.array_equal(gb.steps.cpu().numpy(), alone[k][1]), k
+        assert np.array_equal(gb.winner.cpu().numpy(), alone[k][2]), k
+
+
 def test_gpu_rollout_u_option_overflow(engine):
     """Random-role games (thousands of options per step for the cardinal /
     magician) through k_rollout_u at B = 1024: a draw k >= 64 misses the LDS

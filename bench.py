@@ -8,7 +8,7 @@ to terminal.  One bench step = one launch of the fused rollout kernel
 steps and ranks (seed = base + (step * world + rank) * B + lane), so N GPUs
 play N x 4096 independent games per step (weak scaling, no data-path
 collective).  The K steps are launched round-robin on `--streams` HIP
-streams (default 2, warmed before the timed region): a launch lasts as long
+streams (default 3, warmed before the timed region): a launch lasts as long
 as its longest game, and the next batch's games take the SIMD slots the
 finished games free (tests/test_gpu_parity.py::test_gpu_rollout_streams_overlap
 checks overlapped batches equal batches run alone).  `streams.one_stream`
@@ -224,7 +224,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=4096, help="games per GPU")
     ap.add_argument("--games-per-block", type=int, default=0, help="0 = k_rollout_u (one game per workgroup)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the K timed batches are launched round-robin on (1 = one after another)")
     ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per C++ CPU-baseline leg")
     ap.add_argument("--py-seconds", type=float, default=2.0, help="Python-oracle CPU figure")

@@ -290,8 +290,13 @@ __device__ unsigned long long g_roll_clock[2 * 65536];
 #endif
 
 // The hot loop (default): one game per workgroup (uniform_game), row and
-// MT19937 words in LDS for the whole rollout.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_rollout_u(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
+// MT19937 words in LDS for the whole rollout.  ROLL_WAVES_PER_EU bounds the
+// register budget: 8 -> 64 VGPRs (some spilled to scratch), 8 games resident
+// per SIMD, so a second batch in flight fills the slots.
+#ifndef ROLL_WAVES_PER_EU
+#define ROLL_WAVES_PER_EU 8
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROLL_WAVES_PER_EU))) void k_rollout_u(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
                                                  int max_steps, int32_t* steps_out, int32_t* winner) {
   __shared__ __attribute__((aligned(16))) CitOpt buf[ROLLOUT_BUF ? ROLLOUT_BUF : 1];
 #ifdef ROLL_CLOCK

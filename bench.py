@@ -8,37 +8,55 @@ to terminal.  One bench step = one launch of the fused rollout kernel
 steps and ranks (seed = base + (step * world + rank) * B + lane), so N GPUs
 play N x 4096 independent games per step (weak scaling, no data-path
 collective).  The K steps are launched round-robin on `--streams` HIP
-streams (default 3, warmed before the timed region): a launch lasts as long
-as its longest game, and the next batch's games take the SIMD slots the
-finished games free (tests/test_gpu_parity.py::test_gpu_rollout_streams_overlap
-checks overlapped batches equal batches run alone).  `streams.one_stream`
-replays the same K batches one after another for comparison.
+streams (default 3, warmed before the timed region), so up to
+`config.games_in_flight` = streams x 4096 games are resident at once: a
+launch lasts as long as its longest game, and the next batches' games take
+the SIMD slots the finished games free
+(tests/test_gpu_parity.py::test_gpu_rollout_streams_overlap checks
+overlapped batches equal batches run alone).  `value_one_batch` replays the
+same K batches one after another (one batch resident at a time).
 
 Prints ONE JSON line on rank 0.  `value` = carry_out transitions of all ranks
 / max-over-ranks wall time of the K timed steps.
 
 * `roofline` prices one k_rollout_u launch running alone (the one-stream
-  replay; the PMC children run with --streams 1) by its algorithmic bytes (2 x CIT_GAME_BYTES
-  per transition) over its HIP-event duration against HBM
-  peak; `traffic` is the HBM bytes per launch measured IN THIS RUN by two
-  rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child run of
-  this script (N = 1 only; gfx950 FETCH_SIZE half-count corrected).  Since
-  the kernel keeps each game in LDS, those bytes are far below the
-  algorithmic ones: `roofline.issue` reports what does bound it, from a third
-  --pmc pass of SQ counters: SALU / VALU / LDS instructions per transition,
-  the scalar-issue floor (1 SALU per clock per CU) and the wait fraction.
+  replay; the PMC children run with --streams 1).  The kernel keeps each game
+  in LDS and is bound by instruction issue and per-wave latency, not HBM, so
+  `bound` is "salu-issue": `achieved` = scalar instructions issued per second
+  (SQ_INSTS_SALU from an in-run rocprofv3 --pmc pass over a short child run
+  of this script) against the CU's one scalar issue per clock (`peak`,
+  256 CU x 2.4 GHz), i.e. `frac` = SALU floor / kernel time;
+  `wait_any_frac` (SQ_WAIT_ANY / SQ_WAVE_CYCLES) and `busy_frac` (mean / max
+  game length: one wave runs one game, so a launch lasts as long as its
+  longest game) complete the latency model.  `hbm_notional` keeps SURVEY
+  §8(d)'s HBM figure (2 x CIT_GAME_BYTES algorithmic bytes per transition
+  over the kernel time, against 8 TB/s) and `measured_frac` the counter
+  bytes (FETCH_SIZE + WRITE_SIZE, gfx950 FETCH half-count corrected) over the
+  kernel time against the same peak.  Without the counters (N > 1, or
+  --no-pmc) `bound` falls back to the notional HBM figure.
 * `cpu_baseline` times the build's C++ CPU restatement (the same engine
   headers compiled with g++, build/libcitadels_hostcheck.so) on 1 host core
   and on all the cores this process may use, on rank 0 at N = 1, with nproc
   and the lscpu model; the pure-Python oracle (oracle/) is a secondary
   figure and the reference's own Python is quoted from BASELINE.md (measured
   in the survey container; it cannot travel to the GPU box).
-* `e2e` adds the untimed init: games/s with k_init (seeding + deal) inside
-  the timed region.
-* `roofline.latency`: one wave runs one game, so a launch lasts as long as
-  its longest game; steps_mean / steps_max is the share of the launch a
-  SIMD slot does useful work, and kernel time / steps_max the per-step
-  latency of that game (tools/rollout_clock.py).
+* `e2e` adds the init: the same K batches re-initialised (k_mt_seed_cpython +
+  k_init) and rolled out, init + rollout of batch k on stream k % streams, so
+  the next batch's seeding overlaps the previous batches' rollouts.
+* `cfr_configs` (default on; --no-cfr to skip) measures BASELINE configs 3-5,
+  the MCCFR workloads, each a dict with its own value / unit, the SURVEY
+  §8(d) CFR roofline (bytes per child created over the search time), and a
+  C++ CPU baseline (the same search headers built for the host,
+  cith_cfr_timed, 1 core and all usable cores):
+    3: 1024 positions per GPU, one cfr_train(200) decision each (no NN)
+    4: 4096 positions over the job (4096 / N per GPU), cfr_pred(200, depth 10)
+       with ValueOnlyNN(418, 512) weights from torch.manual_seed(0)
+    5: --cfg5-trees simulate_game trees per GPU at cfr_train(--cfg5-iters)
+       (default 200000, the reference's own setting) through the tree queue,
+       targets pooled with the RCCL all-gather
+  At N = 1, config 3 also carries in-run PMC passes of its search kernel.
+* `--config 3|4|5` makes that config the headline line instead (used for the
+  PMC children and for A/B runs).
 """
 import argparse
 import ctypes as C
@@ -63,8 +81,10 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 N_CU, CLOCK_HZ, SIMD_PER_CU = 256, 2.4e9, 4
+SALU_PEAK = N_CU * CLOCK_HZ  # one scalar instruction per clock per CU
 BASE_SEED = 1_000_000_000
-KERNEL = "k_rollout_u"
+CFR_SEED = 30_000_000        # configs 3-5: positions / trees seeded from here (tools/bench_selfplay.py)
+KERNELS = {2: "k_rollout_u", 3: "k_cfr_decide", 4: "k_cfr_pred_step", 5: "k_cfr_train_slice"}
 # The reference's own Python, BASELINE.md §2 config 1 (survey container, 8-core Xeon).
 REF_PY = {"1_core": 12301, "8_procs": 83869, "unit": "carry_out transitions/s",
           "where": "survey container (BASELINE.md), not this box"}
@@ -111,12 +131,16 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def _hostlib():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import hostcheck
+    return hostcheck.lib()
+
+
 def cpu_baseline(seconds, py_seconds):
     """the build's C++ CPU restatement on 1 core and on all usable
     cores, plus the Python oracle (secondary)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import hostcheck
-    lib = hostcheck.lib()
+    lib = _hostlib()
     lib.cith_rollout_timed.argtypes = [C.c_int, C.c_uint64, C.c_double, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.cith_rollout_timed.restype = C.c_int
     threads = host_threads()
@@ -145,6 +169,40 @@ def cpu_baseline(seconds, py_seconds):
             "reference_python": REF_PY}
 
 
+def cfr_cpu_baseline(config, iters, seconds, node_cap, edge_cap, weights=None):
+    """The C++ restatement of the MCCFR workloads (cith_cfr_timed, the search
+    headers built for the host) on 1 core and on all usable cores."""
+    lib = _hostlib()
+    f = lib.cith_cfr_timed
+    f.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_double, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                  C.c_void_p, C.c_void_p, C.c_void_p]
+    f.restype = C.c_int
+    arr = None
+    if weights is not None:
+        ws = [np.ascontiguousarray(w, np.float32) for w in weights]
+        arr = (C.c_void_p * 8)(*[w.ctypes.data for w in ws])
+    threads = host_threads()
+    legs = {}
+    for name, th in (("1_core", 1), ("all_cores", threads)):
+        d, c, e, w = C.c_longlong(), C.c_longlong(), C.c_longlong(), C.c_double()
+        rc = f(config, iters, C.c_uint64(CFR_SEED + 50_000_000), C.c_double(seconds), th, node_cap, edge_cap, arr,
+               C.byref(d), C.byref(c), C.byref(e), C.byref(w))
+        if rc != 0:
+            raise RuntimeError("cith_cfr_timed(%d) returned %d" % (config, rc))
+        legs[name] = {"value": d.value / w.value, "threads": th, "units": d.value, "carry_outs": c.value,
+                      "carry_out_per_s": c.value / w.value, "error_lanes": e.value, "wall_s": w.value}
+    a = legs["all_cores"]
+    unit = "trees/s" if config == 5 else "decisions/s"
+    return {"value": a["value"], "unit": unit, "cores": a["threads"], "kind": "port",
+            "impl": "cpp-restatement: the search headers (csrc/cit_cfr.h, cit_engine.h) built with g++ -O3 for the "
+                    "host (cith_cfr_timed), one tree per thread" + (", host fp32 value net" if config == 4 else ""),
+            "sample": "%d %s on %d threads x %.0f s, %d on 1 core x %.0f s" % (
+                a["units"], "trees" if config == 5 else "decisions", a["threads"], seconds, legs["1_core"]["units"],
+                seconds),
+            "one_core": legs["1_core"]["value"], "legs": legs, "nproc": os.cpu_count(), "usable_cores": threads,
+            "cpu_model": cpu_model()}
+
+
 def _rows(pattern):
     out = []
     for p in glob.glob(pattern, recursive=True):
@@ -153,15 +211,16 @@ def _rows(pattern):
     return out
 
 
-def _pmc_pass(counters, outdir, timeout_s=150):
+def _pmc_pass(counters, outdir, config=2, timeout_s=150):
     """One rocprofv3 --pmc pass over a short child run of this script (its own
     process group, killed on timeout).  Returns {counter: mean per launch of
-    k_rollout_u} or raises."""
+    the config's kernel} or raises."""
     os.makedirs(outdir, exist_ok=True)
-    cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", outdir, "-o", "run", "--",
-                                              sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2",
-                                              "--warmup", "1", "--streams", "1", "--no-cpu-baseline",
-                                              "--no-pmc"]
+    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(config), "--no-cpu-baseline", "--no-pmc",
+             "--no-cfr"]
+    child += ["--steps", "2", "--warmup", "1", "--streams", "1"] if config == 2 else ["--cfr-reps", "1", "--cfg5-reps",
+                                                                                      "1"]
+    cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", outdir, "-o", "run", "--"] + child
     env = dict(os.environ, TMPDIR="/tmp")
     with open(os.path.join(outdir, "log.txt"), "w") as log:
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
@@ -173,87 +232,73 @@ def _pmc_pass(counters, outdir, timeout_s=150):
             raise RuntimeError("rocprofv3 --pmc %s timed out" % counters)
     if rc != 0:
         raise RuntimeError("rocprofv3 --pmc %s exited %d" % (counters, rc))
+    kernel = KERNELS[config]
     per = {}
     for r in _rows(os.path.join(outdir, "**", "*counter_collection.csv")):
-        if KERNEL in r.get("Kernel_Name", ""):
+        if kernel in r.get("Kernel_Name", ""):
             per.setdefault(r["Counter_Name"], {}).setdefault(r.get("Dispatch_Id", "0"), 0.0)
             per[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
     if not per:
-        raise RuntimeError("no %s rows in the rocprofv3 output" % KERNEL)
-    return {k: sum(v.values()) / len(v) for k, v in per.items()}
+        raise RuntimeError("no %s rows in the rocprofv3 output" % kernel)
+    out = {k: sum(v.values()) / len(v) for k, v in per.items()}
+    out["_launches"] = max(len(v) for v in per.values())
+    return out
 
 
-def pmc_in_run():
+def pmc_in_run(config=2):
     """Three --pmc passes (FETCH_SIZE, WRITE_SIZE, SQ set), each its own child run."""
     base = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
-    out = {"source": "in-run rocprofv3 --pmc, 3 passes over `bench.py --steps 2 --warmup 1` children"}
+    out = {"source": "in-run rocprofv3 --pmc, 3 passes over `bench.py --config %d` children" % config,
+           "kernel": KERNELS[config]}
     try:
-        f = _pmc_pass(["FETCH_SIZE"], os.path.join(base, "fetch"))["FETCH_SIZE"]
-        w = _pmc_pass(["WRITE_SIZE"], os.path.join(base, "write"))["WRITE_SIZE"]
+        f = _pmc_pass(["FETCH_SIZE"], os.path.join(base, "fetch"), config)["FETCH_SIZE"]
+        w = _pmc_pass(["WRITE_SIZE"], os.path.join(base, "write"), config)["WRITE_SIZE"]
         out["fetch_size_kib"] = f
         out["write_size_kib"] = w
         out["hbm_bytes_per_launch"] = 2 * 1024 * f + 1024 * w
-        out["sq"] = _pmc_pass(SQ_SET, os.path.join(base, "sq"))
+        out["sq"] = _pmc_pass(SQ_SET, os.path.join(base, "sq"), config)
     except Exception as e:  # a missing profiler must not cost the bench line
         out["error"] = str(e)[:300]
     return out
 
 
-def issue_roofline(sq, trans_per_launch, kernel_ms):
-    """What bounds k_rollout_u: instruction issue, from the SQ counters (per
-    wave instruction counts; SQ_*_CYCLES in quad-cycles, used only as a ratio)."""
+def issue_roofline(sq, units_per_launch, kernel_ms, unit="transition"):
+    """What bounds a latency-bound kernel: instruction issue, from the SQ
+    counters (per-wave instruction counts; SQ_*_CYCLES used only as a ratio)."""
     if not sq or "SQ_INSTS_SALU" not in sq:
         return None
     salu, valu, lds = sq["SQ_INSTS_SALU"], sq.get("SQ_INSTS_VALU", 0.0), sq.get("SQ_INSTS_LDS", 0.0)
-    salu_floor_ms = salu / (N_CU * CLOCK_HZ) * 1e3                     # 1 scalar issue / clk / CU
-    valu_floor_ms = valu * 4 / (N_CU * SIMD_PER_CU * CLOCK_HZ) * 1e3    # wave64 on SIMD16: 4 clk
-    out = {"bound": "salu-issue", "salu_per_transition": salu / trans_per_launch,
-           "valu_per_transition": valu / trans_per_launch, "lds_per_transition": lds / trans_per_launch,
-           "salu_floor_ms": salu_floor_ms, "valu_floor_ms": valu_floor_ms,
-           "frac": salu_floor_ms / kernel_ms,
-           "model": "floor = SQ_INSTS_SALU / (256 CU x 2.4 GHz x 1 SALU/clk); frac = floor / kernel time"}
+    salu_floor_ms = salu / SALU_PEAK * 1e3                              # 1 scalar issue / clk / CU
+    valu_floor_ms = valu * 2 / (N_CU * SIMD_PER_CU * CLOCK_HZ) * 1e3    # wave64 on SIMD32: 2 clk
+    out = {"salu_per_%s" % unit: salu / units_per_launch, "valu_per_%s" % unit: valu / units_per_launch,
+           "lds_per_%s" % unit: lds / units_per_launch, "salu_floor_ms": salu_floor_ms,
+           "valu_floor_ms": valu_floor_ms, "salu_frac": salu_floor_ms / kernel_ms,
+           "salu_inst_per_s": salu / (kernel_ms * 1e-3),
+           "model": "SALU floor = SQ_INSTS_SALU / (256 CU x 2.4 GHz x 1 SALU/clk); frac = floor / kernel time"}
     if sq.get("SQ_WAVE_CYCLES"):
         out["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0.0) / sq["SQ_WAVE_CYCLES"]
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4096, help="games per GPU")
-    ap.add_argument("--games-per-block", type=int, default=0, help="0 = k_rollout_u (one game per workgroup)")
-    ap.add_argument("--streams", type=int, default=3,
-                    help="HIP streams the K timed batches are launched round-robin on (1 = one after another)")
-    ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per C++ CPU-baseline leg")
-    ap.add_argument("--py-seconds", type=float, default=2.0, help="Python-oracle CPU figure")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 --pmc passes")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="nccl (= RCCL, the real path); gloo only to rehearse N>1 ranks on one GPU")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    n_dev = torch.cuda.device_count()          # does not initialise the GPU
-    # One rank per GPU.  More ranks than GPUs is only a rehearsal: the ranks are
-    # folded onto the visible GPUs and the line says so ("folded").
-    folded = world > max(1, n_dev)
-    if folded and args.dist_backend == "nccl":
-        raise SystemExit("bench.py: WORLD_SIZE=%d > %d visible GPUs; RCCL needs one rank per GPU "
-                         "(use --dist-backend gloo to rehearse folded ranks)" % (world, n_dev))
-
-    # The PMC passes run as child processes before this process touches the GPU.
-    pmc = pmc_in_run() if (world == 1 and not args.no_pmc) else None
-
-    dev = torch.device("cuda", local % max(1, n_dev))
+def _barrier(world):
     if world > 1:
-        torch.cuda.set_device(dev)
-        dist.init_process_group(args.dist_backend)
-    torch.cuda.set_device(dev)
+        dist.barrier()
 
+
+def _reduce(vals, world, dev, maxes=()):
+    """SUM over ranks, except the indices in `maxes` (MAX)."""
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        for i in maxes:
+            t[i] = tmax[i]
+    return [float(x) for x in t]
+
+
+def run_rollout(args, world, rank, dev, n_dev, pmc):
+    """Config 2: the headline.  Returns the bench line (rank 0) or None."""
     from citadels_self_play_amd import layout as L
     from citadels_self_play_amd.engine import GameBatch
 
@@ -280,7 +325,7 @@ def main():
     streams = [stream] if S == 1 else [torch.cuda.Stream(device=dev) for _ in range(S)]
     if S > 1:
         # A stream's first launches set up its hardware queue: warm every stream
-        # with a small rollout of its own (untimed, seeds outside the timed ones).
+        # with a small init + rollout of its own (untimed, seeds outside the timed ones).
         for i, st in enumerate(streams):
             with torch.cuda.stream(st):
                 for _ in range(2):
@@ -288,8 +333,7 @@ def main():
                               games_per_block=args.games_per_block).rollout()
         torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    if world > 1:
-        dist.barrier()
+    _barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k, gb in enumerate(batches[W:]):
@@ -299,119 +343,319 @@ def main():
             gb.rollout()
             evs[k][1].record(st)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    _barrier(world)
     elapsed = time.perf_counter() - t0
 
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     trans_rank = sum(int(gb.steps.sum().item()) for gb in batches[W:])
-    serial = None
+    overlapped_ms = float(np.mean(kernel_ms))
+    # One batch resident at a time: the same K batches re-initialised (untimed)
+    # and replayed one after another on one stream; the roofline prices these
+    # launches (a kernel running alone).
+    el_s, trans_s = elapsed, trans_rank
     if S > 1:
-        # The roofline prices one launch running alone: replay the same K
-        # batches one after another on one stream (re-initialised, untimed init).
         for gb in batches[W:]:
             gb.reset()
         torch.cuda.synchronize()
         sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        _barrier(world)
+        torch.cuda.synchronize()
         ts = time.perf_counter()
         for k, gb in enumerate(batches[W:]):
             sev[k][0].record(stream)
             gb.rollout()
             sev[k][1].record(stream)
         torch.cuda.synchronize()
+        _barrier(world)
         el_s = time.perf_counter() - ts
         trans_s = sum(int(gb.steps.sum().item()) for gb in batches[W:])
-        overlapped_ms = float(np.mean(kernel_ms))
         kernel_ms = [a.elapsed_time(b) for a, b in sev]
-        serial = {"value_rank0": trans_s / el_s, "ms_per_step": el_s / K * 1e3,
-                  "same_transitions": trans_s == trans_rank,
-                  "overlapped_launch_avg_ms": overlapped_ms}
     # the launch lasts as long as its longest game (one wave per game, latency-bound)
     steps_max = float(np.mean([int(gb.steps.max().item()) for gb in batches[W:]]))
     errs = sum(int((gb.errors() != 0).sum().item()) for gb in batches[W:])
     unfinished = sum(int((~gb.terminal()).sum().item()) for gb in batches[W:])
 
-    # End to end: the same K batches re-initialised (k_init: CPython seeding + deal)
-    # and rolled out, init inside the timed region.
+    # End to end: the same K batches re-initialised (k_mt_seed_cpython + k_init)
+    # and rolled out, init inside the timed region; init + rollout of batch k
+    # on stream k % S, so the next batches' seeding overlaps earlier rollouts.
     ie = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    if world > 1:
-        dist.barrier()
+    _barrier(world)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for k, gb in enumerate(batches[W:]):
-        ie[k][0].record(stream)
-        gb.reset()
-        ie[k][1].record(stream)
-        gb.rollout()
+        st = streams[k % S]
+        with torch.cuda.stream(st):
+            ie[k][0].record(st)
+            gb.reset()
+            ie[k][1].record(st)
+            gb.rollout()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    _barrier(world)
     elapsed_e2e = time.perf_counter() - t1
     init_ms = float(np.mean([a.elapsed_time(b) for a, b in ie]))
+    trans_e2e = sum(int(gb.steps.sum().item()) for gb in batches[W:])
 
-    t = torch.tensor([elapsed, float(trans_rank), float(errs), float(unfinished), elapsed_e2e],
-                     dtype=torch.float64, device=dev)
+    elapsed, trans_all, errs_all, unfinished_all, elapsed_e2e, el_s, trans_s_all, trans_e2e_all = _reduce(
+        [elapsed, trans_rank, errs, unfinished, elapsed_e2e, el_s, trans_s, trans_e2e], world, dev, maxes=(0, 4, 5))
+    if rank != 0:
+        return None
+    per_launch_trans = trans_s / K
+    avg_ms = float(np.mean(kernel_ms))
+    alg_bytes = per_launch_trans * 2 * L.GAME_BYTES
+    hbm_achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    issue = issue_roofline(pmc.get("sq") if pmc else None, per_launch_trans, avg_ms)
+    busy = per_launch_trans / B / steps_max
+    hbm_notional = {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_achieved / HBM_PEAK_GBS,
+                    "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_transition": 2 * L.GAME_BYTES,
+                    "model": "SURVEY §8(d): 2 x CIT_GAME_BYTES per transition over the kernel time (the row stays in "
+                             "LDS, so these bytes never reach HBM)"}
+    if issue is not None:
+        roof = {"bound": "salu-issue", "achieved": issue["salu_inst_per_s"] / 1e9, "peak": SALU_PEAK / 1e9,
+                "unit": "G SALU inst/s", "frac": issue["salu_frac"]}
+    else:
+        roof = {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": hbm_achieved / HBM_PEAK_GBS, "note": "no SQ counters in this run: the notional HBM figure"}
+    roof.update({
+        "traffic": traffic, "kernel": KERNELS[2] if args.games_per_block <= 0 else "k_rollout (lanes)",
+        "kernel_avg_ms": avg_ms, "launches": K,
+        "wait_any_frac": issue.get("wait_any_frac") if issue else None, "busy_frac": busy,
+        "hbm_notional": hbm_notional,
+        "measured_gbs": (traffic / (avg_ms * 1e-3) / 1e9) if traffic else None,
+        "measured_frac": (traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+        "issue": issue,
+        "latency": {"bound": "per-wave step latency x longest game",
+                    "steps_mean": per_launch_trans / B, "steps_max_mean_per_launch": steps_max,
+                    "us_per_step_longest_game": avg_ms * 1e3 / steps_max, "mean_over_max": busy},
+        "pmc": pmc})
+    n_gpus = min(world, max(1, n_dev))
+    return {
+        "metric": "Option.carry_out steps/sec (whole node), 6-player batched self-play",
+        "value": trans_all / elapsed,
+        "unit": "carry_out transitions/s",
+        "n_gpus": n_gpus,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: seeded preset games (run_utils.create_game), CPython-MT19937 random policy; "
+                "k_rollout_u is bit-exact with the reference per seed (tests/test_gpu_parity.py)",
+        "config": {"workload": "config2: %d preset 6-player games per batch, uniform random policy to terminal; "
+                               "batches on %d HIP stream(s), up to %d games resident per GPU" % (B, S, S * B),
+                   "games_per_batch": B, "streams": S, "games_in_flight": S * B,
+                   "games_per_block": args.games_per_block,
+                   "rng": "per-game CPython MT19937 (parity mode)", "parallelism": "dp%d" % world},
+        "value_one_batch": trans_s_all / el_s,
+        "transitions_per_step": trans_all / K,
+        "lane_errors": errs_all,
+        "unfinished_lanes": unfinished_all,
+        "roofline": roof,
+        "streams": {"n": S, "one_batch": {"value": trans_s_all / el_s, "ms_per_step": el_s / K * 1e3,
+                                          "same_transitions": trans_s_all == trans_all},
+                    "overlapped_launch_avg_ms": overlapped_ms,
+                    "note": "K batches launched round-robin on n HIP streams; one_batch replays them one after "
+                            "another; the roofline is priced on one launch running alone"},
+        "e2e": {"games_per_s": world * B * K / elapsed_e2e, "transitions_per_s": trans_e2e_all / elapsed_e2e,
+                "init_ms_per_batch": init_ms, "streams": S,
+                "note": "k_mt_seed_cpython + k_init inside the timed region, init + rollout of batch k on stream "
+                        "k %% %d" % S},
+    }
+
+
+def _value_net(dev):
+    from citadels_self_play_amd import models, selfplay
+    torch.manual_seed(0)
+    m = selfplay.broadcast_model(models.ValueOnlyNN(418, 512).to(dev).eval())
+    return models.ValueNet(m, dev)
+
+
+def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
+    """One of BASELINE configs 3-5 (tools/bench_selfplay.py's harness): median
+    of `args.cfr_reps` timed reps after one warm-up.  Returns a dict (rank 0)."""
+    from citadels_self_play_amd import layout as L
+    from citadels_self_play_amd import selfplay
+    from citadels_self_play_amd.engine import GameBatch, pool_caps
+    iters = {3: 200, 4: 200, 5: args.cfg5_iters}[config]
+    per_gpu = {3: 1024, 4: max(1, 4096 // world), 5: args.cfg5_trees}[config]
+    net = _value_net(dev) if config == 4 else None
+    node_cap = {3: 1024, 4: 2048}.get(config)
+    reps = []
+    stream = torch.cuda.current_stream()
+    n_reps = args.cfg5_reps if config == 5 else args.cfr_reps
+    for rep in range(1 + n_reps):
+        warm = rep == 0
+        n = per_gpu if not (warm and config == 5) else min(per_gpu, 64)
+        it = iters if not (warm and config == 5) else min(iters, 2000)
+        seeds = selfplay.shard(n * world, base_seed=CFR_SEED + rep * 1_000_000)
+        if config in (3, 4):
+            b = GameBatch(seeds, preset=True, device=dev)
+            b.advance_random(0, 300)
+            b.seed_numpy()
+        torch.cuda.synchronize()
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        _barrier(world)
+        t0 = time.perf_counter()
+        ev[0].record(stream)
+        rounds, n_targets = 0, 0
+        if config == 3:
+            chosen, stats = b.cfr_decide(it, node_cap=node_cap)
+            term = b.terminal()
+        elif config == 4:
+            chosen, stats, rounds = b.cfr_pred(it, net, max_depth=10, node_cap=node_cap)
+            term = b.terminal()
+        else:
+            b, stats, t = selfplay.simulate_games(seeds, it)
+            f, v = selfplay.all_gather_targets(t["feat"], t["value"])
+            n_targets = int(f.shape[0])
+            term = t["terminal"]
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        _barrier(world)
+        el = time.perf_counter() - t0
+        if warm:
+            continue
+        st = stats.to(dev).to(torch.float64)
+        bad = ((st[:, 4] != 0) & ~term.to(dev)).sum()
+        el_max, units, carry, nodes, edges, errs, terms = _reduce(
+            [el, st.shape[0], st[:, 3].sum(), st[:, 1].sum(), st[:, 2].sum(), bad, term.sum()], world, dev, maxes=(0,))
+        reps.append({"seconds": el_max, "gpu_ms_rank0": ev[0].elapsed_time(ev[1]), "units": units,
+                     "value": units / el_max, "carry_out_per_s": carry / el_max, "nodes": nodes, "edges": edges,
+                     "error_lanes_nonterminal": int(errs), "terminal_positions": int(terms), "leaf_rounds": rounds,
+                     "pooled_targets": n_targets})
+    if rank != 0:
+        return None
+    med = sorted(reps, key=lambda r: r["value"])[len(reps) // 2]
+    S = L.GAME_BYTES
+    # SURVEY §8(d): per child created 2S (row copy) + 2S (transition) + S (determinize) + 24 B per edge slot
+    alg = med["nodes"] * 5 * S + 24.0 * med["edges"]
+    ms = med["seconds"] * 1e3
+    achieved = alg / world / med["seconds"] / 1e9          # per GPU
+    out = {"config": config, "workload": {
+        3: "config3: %d positions per GPU (preset game + U[0,300] random steps), one cfr_train(200) decision each"
+           % per_gpu,
+        4: "config4: %d positions per GPU (4096 over the job), cfr_pred(200, depth 10) + ValueOnlyNN(418,512) "
+           "leaves (torch.manual_seed(0) weights)" % per_gpu,
+        5: "config5: %d simulate_game trees per GPU: create_a_random_game(100) -> cfr_train(%d) -> "
+           "get_all_targets(200), tree queue, targets all-gathered" % (per_gpu, iters)}[config],
+        "value": med["value"], "unit": "trees/s" if config == 5 else "decisions/s",
+        "carry_out_per_s": med["carry_out_per_s"], "reps": len(reps), "median": med,
+        "all_reps_value": [r["value"] for r in reps],
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "kernel": KERNELS[config],
+                     "alg_bytes": alg, "search_ms": ms,
+                     "model": "SURVEY §8(d) CFR expand bytes: 5 x CIT_GAME_BYTES per node created + 24 B per edge "
+                              "slot, over the search's wall time per GPU (the search is a serial latency chain per "
+                              "tree: see issue / DESIGN.md §5)"}}
+    if pmc:
+        sq = pmc.get("sq")
+        launches = (sq or {}).get("_launches", 1)
+        if sq and config == 3:
+            # the child runs one config-3 batch per launch: price per carry_out of that batch
+            carry_per_launch = med["carry_out_per_s"] * med["seconds"] / max(1, world)
+            out["roofline"]["issue"] = issue_roofline(sq, carry_per_launch, med["gpu_ms_rank0"], unit="carry_out")
+        out["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch")
+        out["roofline"]["pmc"] = pmc
+        out["roofline"]["pmc_launches"] = launches
+    if cpu and world == 1 and not args.no_cpu_baseline:
+        w = None
+        if config == 4:
+            from citadels_self_play_amd import models
+            w = [t.numpy() for t in models.fold(_cpu_model())]
+        nc, ec = pool_caps(iters) if config == 5 else (node_cap, 5 * node_cap)
+        try:
+            out["cpu_baseline"] = cfr_cpu_baseline(config, iters, args.cfr_cpu_seconds, nc, ec, w)
+        except Exception as e:
+            out["cpu_baseline"] = {"error": str(e)[:300]}
+    return out
+
+
+def _cpu_model():
+    from citadels_self_play_amd import models
+    torch.manual_seed(0)
+    return models.ValueOnlyNN(418, 512).eval()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
+                    help="headline workload (BASELINE configs; 2 = the metric's own)")
+    ap.add_argument("--batch", type=int, default=4096, help="games per batch per GPU (config 2)")
+    ap.add_argument("--games-per-block", type=int, default=0, help="0 = k_rollout_u (one game per workgroup)")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="HIP streams the K timed batches are launched round-robin on (1 = one after another)")
+    ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per C++ CPU-baseline leg")
+    ap.add_argument("--py-seconds", type=float, default=2.0, help="Python-oracle CPU figure")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 --pmc passes")
+    ap.add_argument("--no-cfr", action="store_true", help="skip the configs 3-5 legs (cfr_configs)")
+    ap.add_argument("--cfr-configs", default="3,4,5")
+    ap.add_argument("--cfr-reps", type=int, default=5, help="timed reps of configs 3 and 4 (median reported)")
+    ap.add_argument("--cfg5-reps", type=int, default=1, help="timed reps of config 5")
+    ap.add_argument("--cfr-cpu-seconds", type=float, default=4.0, help="per C++ CPU-baseline leg of configs 3-5")
+    ap.add_argument("--cfg5-trees", type=int, default=640, help="config 5 trees per GPU")
+    ap.add_argument("--cfg5-iters", type=int, default=200000, help="config 5 cfr_train iterations per tree")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, the real path); gloo only to rehearse N>1 ranks on one GPU")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_dev = torch.cuda.device_count()          # does not initialise the GPU
+    # One rank per GPU.  More ranks than GPUs is only a rehearsal: the ranks are
+    # folded onto the visible GPUs and the line says so ("folded").
+    folded = world > max(1, n_dev)
+    if folded and args.dist_backend == "nccl":
+        raise SystemExit("bench.py: WORLD_SIZE=%d > %d visible GPUs; RCCL needs one rank per GPU "
+                         "(use --dist-backend gloo to rehearse folded ranks)" % (world, n_dev))
+    cfr_list = [] if args.no_cfr or args.config != 2 else [int(c) for c in args.cfr_configs.split(",") if c.strip()]
+
+    # The PMC passes run as child processes before this process touches the GPU.
+    pmc = pmc_in_run(args.config) if (world == 1 and not args.no_pmc) else None
+    cfr_pmc = pmc_in_run(3) if (world == 1 and not args.no_pmc and 3 in cfr_list) else None
+
+    dev = torch.device("cuda", local % max(1, n_dev))
     if world > 1:
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed, elapsed_e2e = float(tmax[0]), float(tmax[4])
-    trans_all, errs_all, unfinished_all = float(t[1]), int(t[2]), int(t[3])
+        torch.cuda.set_device(dev)
+        dist.init_process_group(args.dist_backend)
+    torch.cuda.set_device(dev)
+
+    if args.config == 2:
+        out = run_rollout(args, world, rank, dev, n_dev, pmc)
+    else:
+        c = run_cfr(args.config, args, world, rank, dev, pmc=pmc)
+        out = None
+        if rank == 0:
+            out = {"metric": "MCCFR config %d" % args.config, "value": c["value"], "unit": c["unit"],
+                   "n_gpus": min(world, max(1, n_dev)), "steps": c["reps"], "warmup": 1,
+                   "ms_per_step": c["median"]["seconds"] * 1e3, "higher_is_better": True, "scaling": "weak",
+                   "vs_baseline": None, "dtype": "f64", "data": "synthetic seeded positions",
+                   "config": {"workload": c["workload"], "parallelism": "dp%d" % world},
+                   "roofline": c["roofline"], "cpu_baseline": c.get("cpu_baseline"), "cfr": c}
+    cfr_out = {}
+    for c in cfr_list:
+        try:
+            cfr_out[str(c)] = run_cfr(c, args, world, rank, dev, pmc=cfr_pmc if c == 3 else None)
+        except Exception as e:          # a CFR leg must not cost the headline line
+            cfr_out[str(c)] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
 
     if rank == 0:
-        per_launch_trans = trans_rank / K
-        avg_ms = float(np.mean(kernel_ms))
-        alg_bytes = per_launch_trans * 2 * L.GAME_BYTES
-        achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-        n_gpus = min(world, max(1, n_dev))
-        out = {
-            "metric": "Option.carry_out steps/sec (whole node), 6-player batched self-play",
-            "value": trans_all / elapsed,
-            "unit": "carry_out transitions/s",
-            "n_gpus": n_gpus,
-            "steps": K,
-            "warmup": W,
-            "ms_per_step": elapsed / K * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic: seeded preset games (run_utils.create_game), CPython-MT19937 random policy; "
-                    "k_rollout_u is bit-exact with the reference per seed (tests/test_gpu_parity.py)",
-            "config": {"workload": "config2: %d preset 6-player games per GPU, uniform random policy to terminal"
-                                   % B, "games_per_gpu": B, "games_per_block": args.games_per_block,
-                       "rng": "per-game CPython MT19937 (parity mode)", "parallelism": "dp%d" % world},
-            "transitions_per_step": trans_all / K,
-            "lane_errors": errs_all,
-            "unfinished_lanes": unfinished_all,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": KERNEL if args.games_per_block <= 0 else "k_rollout (lanes)",
-                         "kernel_avg_ms": avg_ms,
-                         "alg_bytes_per_launch": alg_bytes,
-                         "alg_bytes_per_transition": 2 * L.GAME_BYTES,
-                         "measured_gbs": (traffic / (avg_ms * 1e-3) / 1e9) if traffic else None,
-                         "issue": issue_roofline(pmc.get("sq") if pmc else None, per_launch_trans, avg_ms),
-                         "latency": {"bound": "per-wave step latency x longest game",
-                                     "steps_mean": per_launch_trans / B, "steps_max_mean_per_launch": steps_max,
-                                     "us_per_step_longest_game": avg_ms * 1e3 / steps_max,
-                                     "mean_over_max": per_launch_trans / B / steps_max},
-                         "pmc": pmc},
-            "streams": {"n": S, "one_stream": serial,
-                        "note": "K batches launched round-robin on n HIP streams (n = 1: one after another); "
-                                "roofline from one launch running alone"},
-            "e2e": {"games_per_s": world * B * K / elapsed_e2e, "transitions_per_s": trans_all / elapsed_e2e,
-                    "init_ms_per_batch": init_ms,
-                    "note": "k_init (CPython init_by_array seeding + preset deal) inside the timed region"},
-        }
         if folded:
             out["folded"] = True
             out["ranks"] = world
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.py_seconds)
-        else:
-            out["cpu_baseline"] = None
+        if args.config == 2:
+            if world == 1 and not args.no_cpu_baseline:
+                out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.py_seconds)
+            else:
+                out["cpu_baseline"] = None
+        if cfr_list:
+            out["cfr_configs"] = cfr_out
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -563,13 +563,23 @@ class _NodeView:
         the device from the tree's numpy stream: (child node, option)."""
         if live:
             raise ValueError("live decisions come from the root (CFRNode.action_choice(live=True))")
-        b = self.owner._b
+        main = self.owner._b
+        b, j = main.lane_batch(0)            # the tree of a search retried after an overflow lives in its retry batch
         d = b.device
-        node = torch.tensor([self.n], dtype=torch.int32, device=d)
-        edge = torch.zeros(1, dtype=torch.int32, device=d)
-        err = torch.zeros(1, dtype=torch.int32, device=d)
-        _lib.check(b.lib.cit_cfr_action_choice(_ptr(b.pool), 1, b.node_cap, b.edge_cap, _ptr(node), _ptr(b.np_mt),
-                                               _ptr(b.np_idx), _ptr(edge), _ptr(err), _cs()), "cit_cfr_action_choice")
+        node = torch.full((b.B,), -1, dtype=torch.int32, device=d)
+        node[j] = self.n
+        edge = torch.zeros(b.B, dtype=torch.int32, device=d)
+        err = torch.zeros(b.B, dtype=torch.int32, device=d)
+        # the draw comes from the game's numpy stream (the main batch's lane 0)
+        np_mt = torch.zeros((main.np_mt.shape[0], b.B), dtype=main.np_mt.dtype, device=d)
+        np_idx = torch.zeros(b.B, dtype=main.np_idx.dtype, device=d)
+        np_mt[:, j] = main.np_mt[:, 0]
+        np_idx[j] = main.np_idx[0]
+        _lib.check(b.lib.cit_cfr_action_choice(_ptr(b.pool), b.B, b.node_cap, b.edge_cap, _ptr(node), _ptr(np_mt),
+                                               _ptr(np_idx), _ptr(edge), _ptr(err), _cs()), "cit_cfr_action_choice")
+        main.np_mt[:, 0] = np_mt[:, j]
+        main.np_idx[0] = np_idx[j]
+        edge, err = edge[j:j + 1], err[j:j + 1]
         e = int(err.item())
         if e:
             raise_for(e, "action_choice")

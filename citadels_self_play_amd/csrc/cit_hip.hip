@@ -97,44 +97,60 @@ __constant__ CitMTInitTable c_mt_init = cit_mt_init_table();
 
 // CPython random.seed(int) (init_by_array) for 64 games per workgroup, one
 // game per lane: each game's recurrence is serial, so the parallelism is
-// across games.  The first pass reads the constant table, the second reads
-// the first pass's words back from LDS ([624][64], 156 KB: one workgroup per
-// CU); the words then go to HBM structure-of-arrays.  Same stream as
-// mt_seed_cpython (cit_core.h).
+// across games.  The first pass reads the constant table and writes its words
+// straight to the games' HBM streams (structure of arrays [624][B]: a wave's
+// 64 lanes store one coalesced 256-byte line per step); the second pass reads
+// them back from there (L2-resident: written by the same lanes moments
+// before), loads issued a window ahead of the serial chain.  No LDS, so the
+// seeding of the next batch co-resides with rollout waves of the previous
+// ones (bench.py e2e).  Same stream as mt_seed_cpython (cit_core.h).
+#define MT_SEED_AHEAD 16
 __global__ __launch_bounds__(64) void k_mt_seed_cpython(uint32_t* mt, uint32_t* idx, int B, const uint64_t* seeds) {
-  __shared__ uint32_t m[CIT_MT_N * 64];
-  const int l = threadIdx.x;
-  const long g = (long)blockIdx.x * 64 + l;
-  const bool on = g < B;
-  const uint64_t seed = on ? seeds[g] : 0;
+  const long g0 = (long)blockIdx.x * 64 + threadIdx.x;
+  const bool on = g0 < B;
+  const long g = on ? g0 : (long)B - 1;   // an idle lane recomputes the last game and stores nothing
+  const uint64_t seed = seeds[g];
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const int klen = k1 ? 2 : 1;
+  uint32_t* m = mt + g;                   // word i at m[i * B]
   uint32_t prev = c_mt_init.w[0];
   int j = 0;
   // pass 1 (k = 624 steps): i = 1..623 read the table, the 624th (i = 1 again) its own output
+  uint32_t w1 = 0;
   for (int i = 1; i < CIT_MT_N; i++) {
     uint32_t v = (c_mt_init.w[i] ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? k1 : k0) + (uint32_t)j;
-    m[i * 64 + l] = v;
+    if (i == 1) w1 = v;
+    else if (on) m[(long)i * B] = v;
     prev = v;
     j = j + 1 >= klen ? 0 : j + 1;
   }
-  m[l] = prev;
   {
-    uint32_t v = (m[64 + l] ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? k1 : k0) + (uint32_t)j;
-    m[64 + l] = v;
+    uint32_t v = (w1 ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? k1 : k0) + (uint32_t)j;
+    w1 = v;
     prev = v;
   }
-  // pass 2 (623 steps): i = 2..623, then i = 1
-  for (int i = 2; i < CIT_MT_N; i++) {
-    uint32_t v = (m[i * 64 + l] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
-    m[i * 64 + l] = v;
-    prev = v;
+  // pass 2 (623 steps): i = 2..623, then i = 1; words 2..623 come back from HBM / L2
+  __threadfence_block();
+  uint32_t ahead[MT_SEED_AHEAD];
+#pragma unroll
+  for (int k = 0; k < MT_SEED_AHEAD; k++) ahead[k] = m[(long)(2 + k) * B];
+  for (int i0 = 2; i0 < CIT_MT_N; i0 += MT_SEED_AHEAD) {
+#pragma unroll
+    for (int k = 0; k < MT_SEED_AHEAD; k++) {
+      const int i = i0 + k;
+      if (i < CIT_MT_N) {
+        uint32_t v = (ahead[k] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
+        const int ni = i + MT_SEED_AHEAD;
+        if (ni < CIT_MT_N) ahead[k] = m[(long)ni * B];
+        if (on) m[(long)i * B] = v;
+        prev = v;
+      }
+    }
   }
-  m[l] = prev;
-  m[64 + l] = (m[64 + l] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - 1u;
-  m[l] = 0x80000000u;
+  w1 = (w1 ^ ((prev ^ (prev >> 30)) * 1566083941u)) - 1u;
   if (on) {
-    for (int i = 0; i < CIT_MT_N; i++) mt[(long)i * B + g] = m[i * 64 + l];
+    m[0] = 0x80000000u;
+    m[B] = w1;
     idx[g] = CIT_MT_N;
   }
 }

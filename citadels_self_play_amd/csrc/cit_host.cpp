@@ -472,4 +472,140 @@ int cith_rollout_timed(int preset, uint64_t seed0, double seconds, int threads, 
   return (int)errs.load();
 }
 
+// The value net's forward for one feature row on the host (ValueOnlyNN,
+// algorithms/models.py:17-24, eval mode, BatchNorm folded as models.fold
+// does: w = [w1t, b1, w2t, b2, w3t, b3, w4t, b4], [in][out] fp32) followed by
+// square_and_normalize (train_utils.py:143-145).  Timing only: no bitwise
+// claim against the MFMA kernel (the fmaf-chain oracle makes that one).
+static void host_value_net(const float* const* w, const float* x, float* probs) {
+  static const int dims[5] = {CIT_FEAT, 512, 256, 128, 6};
+  float a[512], b[512];
+  const float* in = x;
+  float* bufs[2] = {a, b};
+  for (int layer = 0; layer < 4; layer++) {
+    int ni = dims[layer], no = dims[layer + 1];
+    const float* wt = w[2 * layer];
+    const float* bias = w[2 * layer + 1];
+    float* out = layer == 3 ? probs : bufs[layer & 1];
+    for (int o = 0; o < no; o++) out[o] = bias[o];
+    for (int i = 0; i < ni; i++) {
+      float v = in[i];
+      if (v == 0.0f) continue;
+      const float* row = wt + (long)i * no;
+      for (int o = 0; o < no; o++) out[o] += v * row[o];
+    }
+    if (layer < 3)
+      for (int o = 0; o < no; o++) out[o] = out[o] > 0.0f ? out[o] : 0.0f;
+    in = out;
+  }
+  float s = 0.0f;
+  for (int o = 0; o < 6; o++) s += probs[o] * probs[o];
+  for (int o = 0; o < 6; o++) probs[o] = probs[o] * probs[o] / s;
+}
+
+// CPU baseline of the MCCFR workloads (BASELINE.json configs 3-5, bench.py's
+// cfr legs): `threads` host threads each take seeds seed0, seed0+1, ... (an
+// atomic counter) and run one reference decision per seed until `seconds`
+// have elapsed, with the engine headers built for the host:
+//   config 3: random.seed(s); create_game(); randint(0, 300) random steps;
+//             np.random.seed(s); run_mccfr(game, None, iters)  (cfr_train)
+//   config 4: the same position, run_mccfr(game, model, iters): cfr_pred(iters,
+//             depth 10) with host_value_net leaves (weights w, models.fold)
+//   config 5: random.seed(s); create_a_random_game(100); np.random.seed(s);
+//             run_mccfr(iters, training=True) + get_all_targets(200)
+// Each thread owns one tree pool of (node_cap, edge_cap).  Out: decisions
+// (trees), carry_outs inside the searches, error lanes, wall time.
+int cith_cfr_timed(int config, int iters, uint64_t seed0, double seconds, int threads, int node_cap, int edge_cap,
+                   const float* const* w, long long* out_decisions, long long* out_carry, long long* out_errs,
+                   double* out_wall) {
+  if (threads <= 0 || seconds < 0 || config < 3 || config > 5 || (config == 4 && !w)) return -1;
+  std::atomic<uint64_t> next(seed0);
+  std::atomic<long long> decisions(0), carry(0), errs(0);
+  auto t0 = std::chrono::steady_clock::now();
+  auto deadline = t0 + std::chrono::duration<double>(seconds);
+  const int nb = cfr_nblocks(node_cap), eb = cfr_eblocks(edge_cap);
+  const int64_t pool_bytes = cfr_pool_bytes(node_cap, edge_cap) + cfr_arena_bytes(nb, eb);
+  auto work = [&]() {
+    CitGame* g = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
+    uint8_t* pool = (uint8_t*)malloc((size_t)pool_bytes);
+    std::vector<uint32_t> mt(CIT_MT_N), npmt(CIT_MT_N);
+    std::vector<uint64_t> seer(CIT_SEER_MAX);
+    std::vector<CitOpt> optbuf(CFR_OPT_CAP);
+    std::vector<uint32_t> ring(config == 5 ? 100 * (CIT_GAME_BYTES / 4) : 1);
+    float feat[CIT_FEAT], probs[6] = {};
+    long long my_dec = 0, my_carry = 0, my_errs = 0;
+    while (pool && std::chrono::steady_clock::now() < deadline) {
+      uint64_t seed = next.fetch_add(1);
+      uint32_t idx = 0, npidx = 0;
+      CitMT r;
+      r.mt = mt.data();
+      r.stride = 1;
+      r.pos = 0;
+      r.coop = 0;
+      mt_seed_cpython(r, seed);
+      int pos_ok;
+      if (config == 5) {
+        pos_ok = cit_random_position(*g, r, seer.data(), ring.data(), 100) >= 0;
+      } else {
+        cit_init_game(*g, r, true);
+        int k = (int)mt_randbelow(r, 301u), s = 0;
+        while (s < k && !g->terminal && !g->err) {
+          cit_random_step(*g, r, seer.data());
+          s++;
+        }
+        pos_ok = !g->err;
+      }
+      idx = r.pos;
+      CitMT q;
+      q.mt = npmt.data();
+      q.stride = 1;
+      q.pos = 0;
+      q.coop = 0;
+      mt_init_genrand(q, (uint32_t)seed);
+      npidx = q.pos;
+      cith_cfr_arena_reset(pool, 1, node_cap, edge_cap, nb, eb);
+      int st[5] = {-1, 0, 0, 0, 1};
+      CitOpt chosen;
+      if (pos_ok && config == 4) {
+        CfrState S;
+        memset(&S, 0, sizeof(S));
+        while (cith_cfr_pred_step(g, mt.data(), &idx, npmt.data(), &npidx, seer.data(), 1, iters, 10, pool, node_cap,
+                                  edge_cap, optbuf.data(), &S, probs, feat, &chosen))
+          host_value_net(w, feat, probs);
+        st[3] = S.carry_outs;
+        st[4] = S.err;
+      } else if (pos_ok) {
+        cith_cfr_decide(g, mt.data(), &idx, npmt.data(), &npidx, seer.data(), 1, iters, 0, pool, node_cap, edge_cap,
+                        optbuf.data(), &chosen, st);
+        if (config == 5 && st[0] >= 0 && !st[4]) {
+          int counts[2] = {0, 0}, offs[2] = {0, 0};
+          cith_cfr_target_count(pool, 1, node_cap, edge_cap, &st[0], CFR_TGT_TREE | CFR_TGT_PRUNE, counts);
+          std::vector<int> meta(5 * (size_t)counts[0] + 5);
+          std::vector<float> tf((size_t)CIT_FEAT * counts[0] + 1), of((size_t)CIT_OPT_FEAT * counts[1] + 1);
+          std::vector<double> tv(6 * (size_t)counts[0] + 1), td((size_t)counts[1] + 1);
+          cith_cfr_targets(pool, 1, node_cap, edge_cap, &st[0], CFR_TGT_TREE | CFR_TGT_PRUNE, mt.data(), &idx, offs,
+                           meta.data(), tf.data(), tv.data(), td.data(), of.data());
+        }
+      }
+      my_dec++;
+      my_carry += st[3];
+      my_errs += (!pos_ok || st[4] != 0);
+    }
+    decisions += my_dec;
+    carry += my_carry;
+    errs += my_errs;
+    free(pool);
+    free(g);
+  };
+  std::vector<std::thread> pool;
+  for (int i = 1; i < threads; i++) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  *out_wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  *out_decisions = decisions;
+  *out_carry = carry;
+  *out_errs = errs;
+  return 0;
+}
+
 }  // extern "C"

@@ -100,7 +100,16 @@ __global__ void k_cfr_choose(uint8_t* pool, int B, int node_cap, int edge_cap, c
   T.err = 0;
   int n = node[l];
   int a = -1;
-  if (n < 0 || n >= node_cap || cfr_node(T, n).n_children <= 0) T.err |= CIT_ERR_VALUE;   // choice over []
+  // a node id the tree does not hold (past its node count: an unallocated
+  // block) is rejected before its record is read
+  bool ok = n >= 0 && n < node_cap && T.nbt[n >> CFR_NB_SHIFT] >= 0;
+  if (ok) {   // and an edge run inside the tree's edge blocks
+    const CfrNode& N = cfr_node(T, n);
+    int f = N.first_edge, span = (N.flags & NF_ROLE_PICK) ? CFR_ROLE_EDGE_SLOTS : N.n_children;
+    ok = N.n_children > 0 && f >= 0 && (int64_t)f + span <= edge_cap && T.ebt[f >> CFR_EB_SHIFT] >= 0 &&
+         T.ebt[(f + span - 1) >> CFR_EB_SHIFT] >= 0;
+  }
+  if (!ok) T.err |= CIT_ERR_VALUE;   // choice over []
   else a = cfr_choose(T, n);
   edge_out[l] = T.err ? -1 : a;
   err_out[l] = (int32_t)T.err;

@@ -11,6 +11,7 @@ PyTorch supplies device memory and the stream; the compute is the native
 library.  Every call is asynchronous on torch's current stream.
 """
 import math
+import warnings
 
 import numpy as np
 import torch
@@ -27,6 +28,10 @@ ERR_OVERFLOW = 0x1         # CIT_ERR_OVERFLOW (csrc/cit_core.h)
 EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8"), ("S", "<f8"), ("CS", "<f8")])
 WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])   # role-pick columns (csrc/cit_cfr.h)
 CFR_ROOT_SKIPPED = 1       # CIT_CFR_ROOT_SKIPPED (include/citadels.h)
+# Edge slots a node creation may reserve at once (a role-pick node: 10 edges +
+# 10 three-slot CfrWide records, csrc/cit_cfr.h): an overflowing tree within
+# this of its edge cap counts as cap-limited.
+CFR_EDGE_SLACK = 64
 
 
 def node_arrays(nodes, edges, n):
@@ -188,8 +193,15 @@ class GameBatch:
         over = ((stats[:, 4].to(self.device) & ERR_OVERFLOW) != 0).nonzero().flatten()
         if max_retries <= 0 or over.numel() == 0:
             return chosen, stats
+        # 4x caps when a lane reached its own node / edge cap; the same caps when
+        # only the shared arena ran out (the retry batch's arena holds every
+        # sub-tree's worst case, so a cap-limited lane misread as arena-limited
+        # still grows on its next retry)
+        st = stats[over.to(stats.device)].cpu().numpy()
         (n_used, e_used), (n_cap, e_cap) = self.arena_used()
-        grow = 1 if (n_used > n_cap or e_used > e_cap) else 4    # the shared arena ran out: same tree caps
+        arena_out = n_used > n_cap or e_used > e_cap
+        cap_hit = bool(((st[:, 1] >= self.node_cap - 1) | (st[:, 2] + CFR_EDGE_SLACK >= self.edge_cap)).any())
+        grow = 4 if (cap_hit or not arena_out) else 1
         g, mt, idx, seer, npm, npi, steps = snap
         sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),
                                      seer[over].contiguous(), npm[:, over].contiguous(), npi[over].contiguous())
@@ -360,8 +372,13 @@ class GameBatch:
             if need > avail:
                 nbt, ebt = L.cfr_nblocks(node_cap), L.cfr_eblocks(edge_cap)
                 scale = max(0.0, (avail - per * self.B) / float(need - per * self.B))
+                nb0, eb0 = nb, eb
                 nb, eb = max(nbt, int(nb * scale)), max(ebt, int(eb * scale))
                 need = per * self.B + self.lib.cit_cfr_arena_bytes(nb, eb)
+                warnings.warn("node arena cut to %.0f%% of the requested %d node / %d edge blocks (%d trees): "
+                              "device memory is short, trees that find it exhausted are searched again "
+                              "(slower, same results); use fewer trees per batch to avoid this"
+                              % (100.0 * nb / max(1, nb0), nb0, eb0, self.B), RuntimeWarning, stacklevel=3)
         if have and have < need:
             self.pool = None                        # free the old pool before allocating the new one
             torch.cuda.empty_cache()
@@ -446,16 +463,23 @@ class GameBatch:
         stats = torch.stack([st[:, 8], st[:, 0], st[:, 1], st[:, 3], st[:, 2]], dim=1)
         return chosen, stats, rounds
 
-    def tree(self, lane):
-        """(nodes, edges, rows) numpy views of one lane's search tree (host copy);
-        a lane searched again after a pool overflow is read from its retry batch."""
+    def lane_batch(self, lane):
+        """(batch, lane in it) holding `lane`'s last search tree: the retry
+        sub-batch (recursively) when the lane was searched again after an
+        overflow, else this batch."""
         retry = getattr(self, "_retry", None)
         if retry is not None:
             over = retry[0].cpu().tolist()
             if lane in over:
-                return retry[1].tree(over.index(lane))
-        nodes, edges, rows = L.cfr_tree_bytes(lambda o, n: self.pool[o:o + n].cpu().numpy(), self.B, lane,
-                                              self.node_cap, self.edge_cap)
+                return retry[1].lane_batch(over.index(lane))
+        return self, lane
+
+    def tree(self, lane):
+        """(nodes, edges, rows) numpy views of one lane's search tree (host copy);
+        a lane searched again after a pool overflow is read from its retry batch."""
+        b, lane = self.lane_batch(lane)
+        nodes, edges, rows = L.cfr_tree_bytes(lambda o, n: b.pool[o:o + n].cpu().numpy(), b.B, lane,
+                                              b.node_cap, b.edge_cap)
         return nodes.view(NODE_DT), edges.view(EDGE_DT), rows
 
     # --- single-game pieces of the search, exposed for the object API -------------

@@ -126,7 +126,10 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
     queue=False: consecutive equal chunks, the returned batch then being the
     last chunk's); results are concatenated in seed order either way.
     targets["terminal"] [B] marks the positions that were already over (the
-    reference's run_mccfr raises ValueError on them)."""
+    reference's run_mccfr raises ValueError on them); targets["overflow"] [B]
+    the trees that still overflowed after their retries; targets["chosen"]
+    [B,16] every tree's live decision.  A tree whose search ended in an error
+    (the reference's ValueError, or a surviving overflow) yields no targets."""
     from .engine import pool_bytes
     if node_cap is None:
         node_cap, ec = pool_caps(iters)
@@ -159,8 +162,10 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
         b.seed_numpy()
         term = b.terminal()
         chosen, stats = b.cfr_decide(iters, node_cap=node_cap, edge_cap=edge_cap)
-        t = b.cfr_targets(stats[:, 0], mode=0)
+        t = b.cfr_targets(_roots_for_targets(stats), mode=0)
         t["terminal"] = term
+        t["overflow"] = _overflowed(stats)
+        t["chosen"] = chosen
         parts.append((stats, t))
         if log is not None:
             used, cap = b.arena_used()
@@ -299,6 +304,7 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     stats = torch.zeros((S, 5), dtype=torch.int32, device=dev)
     running = torch.zeros(1, dtype=torch.int32, device=dev)
     out_stats = torch.zeros((Q, 5), dtype=torch.int32, device=dev)
+    out_chosen = torch.zeros((Q, 16), dtype=torch.uint8, device=dev)
     slot_q = torch.arange(S, device=dev)         # queue index held by each slot (-1: idle)
     parts, nxt, n_slices, n_done = [], S, 0, 0
     ticks = max(1, int(slice_seconds * 1e8))
@@ -325,7 +331,8 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
             qs = slot_q[done]
             out_stats[qs] = stats[done]
             roots = torch.full((S,), -1, dtype=torch.int32, device=dev)
-            roots[done] = stats[done, 0]
+            roots[done] = _roots_for_targets(stats[done])
+            out_chosen[qs] = chosen[done]
             parts.append((sb._cfr_targets(roots, 0), done, qs))
             src.scatter(sb.subset(done), qs)
             sb.release(done)
@@ -353,15 +360,33 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
         g, mt, idx, seer, npm, npi, steps = snap
         sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),
                                      seer[over].contiguous(), npm[:, over].contiguous(), npi[over].contiguous())
-        _, st2 = sub.cfr_decide(iters, node_cap, edge_cap)
+        c2, st2 = sub.cfr_decide(iters, node_cap, edge_cap)
         out_stats[over] = st2
-        sub_roots = st2[:, 0].to(torch.int32)
-        extra = sub.cfr_targets(sub_roots, 0)
+        out_chosen[over] = c2
+        extra = sub.cfr_targets(_roots_for_targets(st2), 0)
         parts.append((extra, torch.arange(sub.B, device=dev), over))
         src.scatter(sub, over)
     t = _assemble_targets(parts, Q, exclude=over)
     t["terminal"] = term
+    t["overflow"] = _overflowed(out_stats)
+    t["chosen"] = out_chosen
     return src, out_stats, t
+
+
+def _overflowed(stats):
+    """Lanes whose search still carries CIT_ERR_OVERFLOW after its retries."""
+    from .engine import ERR_OVERFLOW
+    return (stats[:, 4] & ERR_OVERFLOW) != 0
+
+
+def _roots_for_targets(stats):
+    """Root ids for cfr_targets with every lane whose search ended in an error
+    set to -1, so it yields no targets: a reference ValueError ends
+    simulate_game before get_all_targets, and a pool overflow that survived
+    its retries is a truncated search (the reference's search has no pool)."""
+    roots = stats[:, 0].to(torch.int32).clone()
+    roots[(stats[:, 4] != 0).to(roots.device)] = -1
+    return roots
 
 
 def _assemble_targets(parts, n, exclude=None):
@@ -415,7 +440,7 @@ def concat_targets(ts, sizes):
         lane0 += n
         row0 += t["dist"].shape[0]
     out = {"meta": torch.cat(metas)}
-    for k in ("feat", "value", "dist", "opt_feat", "counts", "terminal"):
+    for k in ("feat", "value", "dist", "opt_feat", "counts", "terminal", "overflow", "chosen"):
         if all(k in t for t in ts):
             out[k] = torch.cat([t[k] for t in ts])
     return out

@@ -16,6 +16,17 @@ full target tuples are written per rank in the reference's pickle layout
 search in the training phases does not change the search (training=True uses
 no predictions, deep_mccfr.py:119-126,279), so every phase runs the same
 device search.
+
+Error semantics (--on-error).  A reference tree whose search raises (a
+ValueError from np.random.choice over an empty or NaN strategy row, or
+run_mccfr on an already-terminal position) propagates out of Pool.starmap and
+ends the run: get_mccfr_targets catches only RanOutOfMemory
+(train_from_scratch.py:56-63).  `--on-error raise` reproduces that (a
+TreeError, a ValueError, on every rank).  The default `drop` keeps going
+without those trees and logs per round how many were dropped and why
+(reference value errors, terminal positions, and pool overflows that
+survived every retry, which have no reference counterpart); none of them
+contributes targets.
 """
 import argparse
 import os
@@ -28,8 +39,32 @@ from . import selfplay
 from .models import ValueOnlyNN
 
 
+class TreeError(ValueError):
+    """--on-error raise: a simulate_game tree ended in one of the reference's
+    exceptions (train_from_scratch.py:56-63 catches only RanOutOfMemory, so
+    the reference's data generation stops there)."""
+
+
+def lane_errors(stats, t, seeds):
+    """Per-round error accounting: (value_errors, overflow, terminal, first
+    failing seed).  `value_errors` are trees that raised one of the reference's
+    exceptions in the search (CIT_ERR_* other than the pool overflow);
+    `overflow` trees outgrew their node pools after every retry (no reference
+    counterpart); `terminal` positions were already over (run_mccfr raises on
+    them in the reference)."""
+    from .engine import ERR_OVERFLOW
+    err = stats[:, 4].cpu()
+    term = t["terminal"].cpu()
+    over = (err & ERR_OVERFLOW) != 0
+    value = (err != 0) & ~over & ~term
+    bad = (err != 0) | term
+    first = int(seeds[int(bad.nonzero()[0])]) if bool(bad.any()) else None
+    return int(value.sum()), int(over.sum()), int(term.sum()), first
+
+
 def collect(rank, world, args, phase, min_targets, log):
     feats, values, tuples = [], [], []
+    dropped = {"value": 0, "overflow": 0, "terminal": 0}
     pooled = 0
     rnd = 0
     while pooled < min_targets:
@@ -37,18 +72,30 @@ def collect(rank, world, args, phase, min_targets, log):
         seeds = selfplay.shard(args.games_per_gpu * world, base_seed=base)
         t0 = time.time()
         b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap, log=log)
+        n_value, n_over, n_term, first = lane_errors(stats, t, seeds)
+        if args.on_error == "raise":
+            bad = torch.tensor([0 if first is None else 1], device=stats.device)
+            if world > 1:
+                torch.distributed.all_reduce(bad)          # every rank stops together
+            if int(bad.item()):
+                raise TreeError("simulate_game raised in the search (first failing seed on this rank: %s; "
+                                "%d value errors, %d terminal positions, %d pool overflows)"
+                                % (first, n_value, n_term, n_over))
         f, v = selfplay.all_gather_targets(t["feat"], t["value"])
         feats.append(f.cpu())
         values.append(v.cpu())
         if args.save_tuples:
             tuples += selfplay.targets_to_tuples(t)
         pooled += f.shape[0]
-        term = t["terminal"].to(stats.device)
-        errs = int(((stats[:, 4] != 0) & ~term).sum())
-        log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), %d lanes with errors, "
-            "%d already-terminal positions, %.1fs"
-            % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, errs, int(term.sum()), time.time() - t0))
+        dropped["value"] += n_value
+        dropped["overflow"] += n_over
+        dropped["terminal"] += n_term
+        log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), dropped trees on rank %d: %d value "
+            "errors (the reference's ValueError), %d already-terminal positions, %d pool overflows, %.1fs"
+            % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, rank, n_value, n_term, n_over,
+               time.time() - t0))
         rnd += 1
+    collect.dropped = dropped
     return torch.cat(feats), torch.cat(values), tuples
 
 
@@ -69,6 +116,10 @@ def main(argv=None):
     ap.add_argument("--out", default=".")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--save-tuples", action="store_true")
+    ap.add_argument("--on-error", choices=("drop", "raise"), default="drop",
+                    help="a tree whose search raises one of the reference's exceptions (ValueError: an empty or NaN "
+                         "choice; a terminal position): drop it and count it (default), or stop the run as the "
+                         "reference does (train_from_scratch.py:56-63 catches only RanOutOfMemory)")
     args = ap.parse_args(argv)
     rank, world, dev = selfplay.init_distributed()
 
@@ -87,6 +138,7 @@ def main(argv=None):
     plan = [("pretrain", args.pretrain_targets, 0.3703517140136571)] + \
         [("train%d" % u, args.train_targets, 0.02) for u in range(args.phases)]
     model = ValueOnlyNN(418, 512)
+    log("error policy: --on-error %s" % args.on_error)
     for phase, (name, need, lr) in enumerate(plan):
         folder = os.path.join(args.out, name)
         feat, value, tuples = collect(rank, world, args, phase, need, log)

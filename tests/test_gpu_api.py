@@ -106,11 +106,15 @@ def test_api_setup_game_matches_reference():
             break
 
 
-def test_api_cfrnode_constructor_skip_and_live_false_sampler():
+@pytest.mark.parametrize("node_cap", [None, 64])
+def test_api_cfrnode_constructor_skip_and_live_false_sampler(node_cap):
     """CFRNode(game) runs skip_false_choice on `game` in the constructor
     (deep_mccfr.py:19-20); after run_mccfr's search, action_choice(live=False)
     draws children with the in-search sampler from the tree's numpy stream
-    (:67-91) -- both against the oracle's Tree / Node.choose."""
+    (:67-91) -- both against the oracle's Tree / Node.choose.  node_cap=64
+    forces every search to overflow its pool and be searched again (twice:
+    64 -> 256 -> 1024 nodes), so the sampler must read the retry batch's
+    tree (a node id past the overflowed tree would be an unallocated block)."""
     import cfr_oracle as CO
     st = api.default_stream()
     done = 0
@@ -127,13 +131,15 @@ def test_api_cfrnode_constructor_skip_and_live_false_sampler():
             if options[st.randint(0, len(options) - 1)].carry_out(g):
                 break
         assert canon.canon_game(g.packed()) == O.canon(og), seed
-        node = api.CFRNode(g, g.gamestate.player_id)
+        node = api.CFRNode(g, g.gamestate.player_id, node_cap=node_cap)
         og.nprng = npr
         tr = CO.Tree(og, og.gs.pid, np_rng=npr)          # its root Node runs skip_forced on og
         assert canon.canon_game(g.packed()) == O.canon(og), seed
         node.cfr_train(max_iterations=200)
         tr.cfr_train(200)
         assert node.node_count == tr.count and node.carry_outs == tr.carry_outs, seed
+        if node_cap is not None:
+            assert node._b._retry is not None and node._b.lane_batch(0)[0] is not node._b, seed
         _, chosen = node.action_choice(live=True)
         _, ochosen = tr.root.choose(live=True)
         assert chosen.name == ochosen.name, seed

@@ -9,7 +9,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-KEYS = ("meta", "feat", "value", "dist", "opt_feat", "counts", "terminal")
+KEYS = ("meta", "feat", "value", "dist", "opt_feat", "counts", "terminal", "overflow", "chosen")
 
 
 def _same(a, b):

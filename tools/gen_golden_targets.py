@@ -51,8 +51,10 @@ def case(seed, iters):
     gopt.option.carry_out = counting
     try:
         chosen, root = run_mccfr(g, model=None, max_iterations=iters, training=True)
-    except Exception as e:           # a terminal position: action_choice on a childless root
+    except Exception as e:           # a terminal position, or the reference's ValueErrors
         rec["error"] = type(e).__name__
+        rec["message"] = str(e)
+        rec["carry_outs"] = counter[0]
         return rec
     finally:
         gopt.option.carry_out = orig
@@ -76,9 +78,37 @@ def case(seed, iters):
 
 def main():
     """python tools/gen_golden_targets.py [ITERS N_SEEDS]: targets2000.json.gz (16
-    seeds) by default; targets20000.json.gz = cfr_train(20000), 4 seeds."""
+    seeds) by default; targets20000.json.gz = cfr_train(20000), 4 seeds.
+
+    python tools/gen_golden_targets.py ITERS --seeds S1,S2,... [--out NAME]: the
+    listed seeds only, one record per line to NAME.part (so seeds can run in
+    separate processes), then --merge NAME joins the parts in seed order.
+    targets200000.json.gz (the reference's own train_from_scratch setting,
+    train_from_scratch.py:39,45,58): seeds 30000000, 30000001 (error-free),
+    30000012 (ValueError after 1 carry_out) and 30000017 (ValueError deep in
+    the search)."""
     os.makedirs(OUT, exist_ok=True)
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+    if "--merge" in sys.argv:
+        name = sys.argv[sys.argv.index("--merge") + 1]
+        recs = []
+        for fn in sorted(os.listdir(OUT)):
+            if fn.startswith(name + ".") and fn.endswith(".part"):
+                with open(os.path.join(OUT, fn)) as f:
+                    recs += [json.loads(line) for line in f if line.strip()]
+        recs.sort(key=lambda r: r["seed"])
+        with gzip.open(os.path.join(OUT, name), "wt") as f:
+            json.dump(recs, f, separators=(",", ":"))
+        return
+    if "--seeds" in sys.argv:
+        seeds = [int(x) for x in sys.argv[sys.argv.index("--seeds") + 1].split(",")]
+        name = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else "targets%d.json.gz" % iters
+        for s in seeds:
+            rec = case(s, iters)
+            print(s, rec.get("error"), rec.get("nodes"), len(rec.get("targets", [])), flush=True)
+            with open(os.path.join(OUT, "%s.%d.part" % (name, s)), "w") as f:
+                f.write(json.dumps(rec, separators=(",", ":")) + "\n")
+        return
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     recs = []
     for s in range(n):

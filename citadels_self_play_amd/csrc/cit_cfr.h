@@ -69,11 +69,22 @@ static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
 // (a tree takes what it uses, not its worst case: a cfr_train(200000) tree
 // averages ~270k nodes against a ~650k-node maximum):
 //   per tree l (cfr_pool_bytes each): int32 node-block table [nblocks(node_cap)]
-//     | int32 edge-block table [eblocks(edge_cap)] | pad to 16 B
+//     | int32 edge-block table [eblocks(edge_cap)] | pad to 16 B | base row
+//     (CIT_GAME_BYTES) | scratch row (CIT_GAME_BYTES)
 //   arena (at B * cfr_pool_bytes): CfrArena header (64 B) | free-block rings
 //     uint32 [n_cap] + [e_cap] (padded to 16 B) | node records [n_cap
-//     blocks][CFR_NB] | node game rows [n_cap blocks][CFR_NB] (16-byte
-//     aligned, copied as 16-byte words) | edges [e_cap blocks][CFR_EB]
+//     blocks][CFR_NB] | node row slots [n_cap blocks][CFR_NB] (16-byte
+//     aligned) | edges [e_cap blocks][CFR_EB]
+// Row slots (the arena's row_cap, cfr_row_slot_bytes): row_cap 0 stores each
+// node's game row raw (CIT_GAME_BYTES); row_cap K > 0 stores it as a diff
+// against the tree's base row (its root game as first created): a header of
+// CFR_ROW_HDR words (bit d of the 388-bit mask in words 0..12 = dword d differs
+// from the base; word 13 the count) and then the differing dwords in index
+// order, at most K.  A cfr_train(200000) node differs from its root in ~70 of
+// 388 dwords (max ~100 measured), so K = 128 halves a node's bytes; a row
+// with more than K differing dwords stops the tree with CIT_ERR_OVERFLOW and
+// the tree is searched again with raw rows (engine.py's retry): the slot size
+// never changes a result.
 // A block is taken from its free ring (blocks released by finished trees,
 // cit_cfr_arena_release) or, when that is empty, from the never-used rest.
 // Node id n lives in block nbt[n >> CFR_NB_SHIFT] at slot n & (CFR_NB - 1);
@@ -87,8 +98,13 @@ static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
 struct CfrArena {                             // 64 B, written by cit_cfr_arena_reset
   uint32_t n_next, n_cap, e_next, e_cap;      // never-used blocks handed out / capacity
   uint32_t n_head, n_tail, e_head, e_tail;    // free rings: taken / released counts (mod cap)
-  uint32_t pad[8];
+  uint32_t row_cap;                           // row slot format (0: raw rows)
+  uint32_t pad[7];
 };
+#define CFR_ROW_W (CIT_GAME_BYTES / 4)        // 388 dwords
+#define CFR_ROW_HDR 16                        // header words of a diff row slot
+#define CFR_ROW_MASKW 13                      // mask words (388 bits)
+#define CFR_ROW_CAP_MAX 368                   // a diff slot must stay below a raw row
 static_assert(sizeof(CfrArena) == 64, "CfrArena layout");
 
 struct CfrTree {
@@ -101,6 +117,10 @@ struct CfrTree {
   int32_t* nbt_hbm;                    // the tree's tables in the pool
   int32_t* ebt_hbm;
   int node_cap, edge_cap;
+  int row_cap;                         // the arena's row slot format (0: raw rows)
+  int64_t row_slot;                    // bytes per row slot
+  uint32_t* base_hbm;                  // the tree's base row (diff rows) in the pool
+  uint32_t* scratch_hbm;               // one row of scratch per tree in the pool
   int n_nodes, n_edges;
   int n_eblk;                          // edge blocks held
   int orig;
@@ -119,14 +139,23 @@ struct CfrTree {
 
 CIT_HD int cfr_nblocks(int node_cap) { return (node_cap + CFR_NB - 1) >> CFR_NB_SHIFT; }
 CIT_HD int cfr_eblocks(int edge_cap) { return (edge_cap + CFR_EB - 1) >> CFR_EB_SHIFT; }
-CIT_HD int64_t cfr_pool_bytes(int node_cap, int edge_cap) {   // per tree: its two block tables
+CIT_HD int64_t cfr_tables_bytes(int node_cap, int edge_cap) {   // a tree's two block tables, padded
   return ((int64_t)4 * (cfr_nblocks(node_cap) + cfr_eblocks(edge_cap)) + 15) & ~(int64_t)15;
 }
-CIT_HD int64_t cfr_node_block_bytes() { return (int64_t)CFR_NB * (int64_t)(sizeof(CfrNode) + CIT_GAME_BYTES); }
+CIT_HD int64_t cfr_pool_bytes(int node_cap, int edge_cap) {   // per tree: tables, base row, scratch row
+  return cfr_tables_bytes(node_cap, edge_cap) + 2 * (int64_t)CIT_GAME_BYTES;
+}
+CIT_HD int cfr_row_cap_ok(int row_cap) { return row_cap == 0 || (row_cap > 0 && row_cap <= CFR_ROW_CAP_MAX && !(row_cap & 3)); }
+CIT_HD int64_t cfr_row_slot_bytes(int row_cap) {
+  return row_cap > 0 ? (int64_t)4 * (CFR_ROW_HDR + row_cap) : (int64_t)CIT_GAME_BYTES;
+}
+CIT_HD int64_t cfr_node_block_bytes(int row_cap = 0) {
+  return (int64_t)CFR_NB * ((int64_t)sizeof(CfrNode) + cfr_row_slot_bytes(row_cap));
+}
 CIT_HD int64_t cfr_ring_bytes(int64_t n_blocks, int64_t e_blocks) { return (4 * (n_blocks + e_blocks) + 15) & ~(int64_t)15; }
-CIT_HD int64_t cfr_arena_bytes(int n_blocks, int e_blocks) {
-  return (int64_t)sizeof(CfrArena) + cfr_ring_bytes(n_blocks, e_blocks) + (int64_t)n_blocks * cfr_node_block_bytes() +
-         (int64_t)e_blocks * CFR_EB * (int64_t)sizeof(CfrEdge);
+CIT_HD int64_t cfr_arena_bytes(int n_blocks, int e_blocks, int row_cap = 0) {
+  return (int64_t)sizeof(CfrArena) + cfr_ring_bytes(n_blocks, e_blocks) +
+         (int64_t)n_blocks * cfr_node_block_bytes(row_cap) + (int64_t)e_blocks * CFR_EB * (int64_t)sizeof(CfrEdge);
 }
 // Binds tree l of a B-tree pool; the arena's capacities come from its header.
 CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, int B, long l, int node_cap, int edge_cap) {
@@ -136,12 +165,16 @@ CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, int B, long l, int node_cap
   T.ebt_hbm = tbl + cfr_nblocks(node_cap);
   T.nbt = T.nbt_hbm;
   T.ebt = T.ebt_hbm;
+  T.base_hbm = reinterpret_cast<uint32_t*>(pool + per * (int64_t)l + cfr_tables_bytes(node_cap, edge_cap));
+  T.scratch_hbm = T.base_hbm + CFR_ROW_W;
   uint8_t* a = pool + per * (int64_t)B;
   T.arena = reinterpret_cast<CfrArena*>(a);
   int64_t ncap = T.arena->n_cap, ecap = T.arena->e_cap;
+  T.row_cap = (int)T.arena->row_cap;
+  T.row_slot = cfr_row_slot_bytes(T.row_cap);
   T.node_base = a + sizeof(CfrArena) + cfr_ring_bytes(ncap, ecap);
   T.row_base = T.node_base + ncap * CFR_NB * (int64_t)sizeof(CfrNode);
-  T.edge_base = T.row_base + ncap * CFR_NB * (int64_t)CIT_GAME_BYTES;
+  T.edge_base = T.row_base + ncap * CFR_NB * T.row_slot;
   T.node_cap = node_cap;
   T.edge_cap = edge_cap;
 }
@@ -213,7 +246,6 @@ CIT_HD CitOpt cfr_uopt(const CitOpt& o) { return o; }
 #if defined(__HIPCC__)
 struct CfrLds {
   uint32_t w[2][CIT_GAME_BYTES / 4];
-  int32_t nbt[CFR_TBL_MAX], ebt[CFR_TBL_MAX];     // the tree's block tables
   CitOpt lbuf[CFR_LBUF];
   double sbuf[CFR_OPT_CAP], cbuf[CFR_OPT_CAP];   // update_strategy: S, CS of node `cnode`
   uint32_t py[CIT_MT_N], np[CIT_MT_N];
@@ -223,7 +255,18 @@ struct CfrLds {
   uint8_t tmp[CIT_SAMPLE_SCRATCH];
 };
 static __shared__ __attribute__((aligned(16))) CfrLds cfr_ls;
+// Dynamic LDS of a search launch (sized per launch, cfr_dyn_lds_bytes): the
+// tree's base row (diff row slots), then its two block tables interleaved
+// (node-block entry i at [2i], edge-block entry i at [2i + 1]) so both start
+// at fixed addresses whatever the capacities; a tree's tables hold
+// max(nblocks, eblocks) entries each (2 at configs 3/4, 172 at
+// cfr_train(200000)) instead of a fixed CFR_TBL_MAX.
+extern __shared__ __attribute__((aligned(16))) uint32_t cfr_dyn[];
 #endif
+CIT_HD int64_t cfr_dyn_lds_bytes(int node_cap, int edge_cap) {
+  int nb = cfr_nblocks(node_cap), eb = cfr_eblocks(edge_cap);
+  return 4 * ((int64_t)CFR_ROW_W + 2 * (int64_t)(nb > eb ? nb : eb));
+}
 #if CIT_WAVE
 #define CFR_T(T_in) (cfr_ls.T)
 #define CFR_S(S_in) (cfr_ls.S)
@@ -273,24 +316,33 @@ CIT_HD int cfr_take_block(CfrArena* A, int edge) {
   return r;
 }
 
-// The block tables: LDS (fixed addresses) in a device search, else the pool's.
+// The block tables: LDS (fixed addresses, cfr_dyn) in a device search, else
+// the pool's.  Entry i of the node- / edge-block table.
 #if CIT_WAVE
-__device__ __forceinline__ int32_t* cfr_nbt(const CfrTree&) { return cfr_ls.nbt; }
-__device__ __forceinline__ int32_t* cfr_ebt(const CfrTree&) { return cfr_ls.ebt; }
+__device__ __forceinline__ int32_t& cfr_nbt_at(const CfrTree&, int i) {
+  return reinterpret_cast<int32_t*>(cfr_dyn + CFR_ROW_W)[2 * i];
+}
+__device__ __forceinline__ int32_t& cfr_ebt_at(const CfrTree&, int i) {
+  return reinterpret_cast<int32_t*>(cfr_dyn + CFR_ROW_W)[2 * i + 1];
+}
+__device__ __forceinline__ const uint32_t* cfr_base(const CfrTree&) { return cfr_dyn; }
+__device__ __forceinline__ uint32_t* cfr_base_w(const CfrTree&) { return cfr_dyn; }
 #else
-CIT_HD int32_t* cfr_nbt(const CfrTree& T) { return T.nbt; }
-CIT_HD int32_t* cfr_ebt(const CfrTree& T) { return T.ebt; }
+CIT_HD int32_t& cfr_nbt_at(const CfrTree& T, int i) { return T.nbt[i]; }
+CIT_HD int32_t& cfr_ebt_at(const CfrTree& T, int i) { return T.ebt[i]; }
+CIT_HD const uint32_t* cfr_base(const CfrTree& T) { return T.base_hbm; }
+CIT_HD uint32_t* cfr_base_w(const CfrTree& T) { return T.base_hbm; }
 #endif
 
-// node n's record, edge e (a run of edges continues from it), node n's row
+// node n's record, edge e (a run of edges continues from it), node n's row slot
 CIT_HD int64_t cfr_node_slot(const CfrTree& T, int n) {
-  return (int64_t)cfr_nbt(T)[n >> CFR_NB_SHIFT] * CFR_NB + (n & (CFR_NB - 1));
+  return (int64_t)cfr_nbt_at(T, n >> CFR_NB_SHIFT) * CFR_NB + (n & (CFR_NB - 1));
 }
 CIT_HD CfrNode& cfr_node(const CfrTree& T, int n) {
   return *reinterpret_cast<CfrNode*>(cfr_glb(T.node_base) + cfr_node_slot(T, n) * (int64_t)sizeof(CfrNode));
 }
 CIT_HD CfrEdge* cfr_edge(const CfrTree& T, int e) {
-  int64_t slot = (int64_t)cfr_ebt(T)[e >> CFR_EB_SHIFT] * CFR_EB + (e & (CFR_EB - 1));
+  int64_t slot = (int64_t)cfr_ebt_at(T, e >> CFR_EB_SHIFT) * CFR_EB + (e & (CFR_EB - 1));
   return reinterpret_cast<CfrEdge*>(cfr_glb(T.edge_base) + slot * (int64_t)sizeof(CfrEdge));
 }
 // the [6]-wide regret / strategy columns of role-pick child a
@@ -298,7 +350,7 @@ CIT_HD CfrWide* cfr_wide(const CfrTree& T, int first_edge) {
   return reinterpret_cast<CfrWide*>(cfr_edge(T, first_edge) + CFR_ROLE_CHILDREN);
 }
 CIT_HD uint32_t* row_of(const CfrTree& T, int id) {
-  return reinterpret_cast<uint32_t*>(cfr_glb(T.row_base) + cfr_node_slot(T, id) * (int64_t)CIT_GAME_BYTES);
+  return reinterpret_cast<uint32_t*>(cfr_glb(T.row_base) + cfr_node_slot(T, id) * T.row_slot);
 }
 CIT_HD uint32_t* w_row(const CfrTree& T, int which) { return reinterpret_cast<uint32_t*>(&cfr_w(T, which)); }
 
@@ -392,6 +444,128 @@ CIT_HD void copy_row(const CfrTree& T, uint32_t* dst, const uint32_t* src) {
   for (int i = CFR_LANE; i < CIT_GAME_BYTES / 4; i += CFR_TEAM) dst[i] = src[i];
 #endif
   CFR_SYNC();
+}
+
+// Node row slots (see the pool layout above): row_load = the node's game row
+// into dst (a working row in LDS, a scratch row, or a games[] row in HBM);
+// row_store = working row src into the node's slot (diff rows: against the
+// tree's base row; more than row_cap differing dwords -> CIT_ERR_OVERFLOW).
+#if CIT_WAVE
+__device__ __forceinline__ uint32_t cfr_mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+#endif
+CIT_HD void row_load(const CfrTree& T, uint32_t* dst, int id) {
+  const uint32_t* s = row_of(T, id);
+  if (cfr_u(T.row_cap) == 0) {
+    copy_row(T, dst, s);
+    return;
+  }
+  const uint32_t* base = cfr_base(T);
+  CFR_SYNC();
+#if CIT_WAVE
+  {   // lanes 0..12 hold the mask words; chunk j = dwords 64j..64j+63 on the 64 lanes
+    const int l = CFR_LANE;
+    const uint32_t mw = l < CFR_ROW_MASKW ? s[l] : 0u;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < (CFR_ROW_W + 63) / 64; j++) {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mw, 2 * j);
+      const uint32_t hi = 2 * j + 1 < CFR_ROW_MASKW ? (uint32_t)__builtin_amdgcn_readlane((int)mw, 2 * j + 1) : 0u;
+      const uint64_t m = ((uint64_t)hi << 32) | lo;
+      const int d = 64 * j + l;
+      if (d < CFR_ROW_W) dst[d] = ((m >> l) & 1) ? s[CFR_ROW_HDR + acc + cfr_mbcnt(m)] : base[d];
+      acc += (uint32_t)__popcll(m);
+    }
+  }
+#else
+  {
+    uint32_t k = 0;
+    for (int d = 0; d < CFR_ROW_W; d++)
+      dst[d] = ((s[d >> 5] >> (d & 31)) & 1) ? s[CFR_ROW_HDR + k++] : base[d];
+  }
+#endif
+  CFR_SYNC();
+}
+CIT_HD void row_store(CfrTree& T, int id, const uint32_t* src) {
+  uint32_t* s = row_of(T, id);
+  if (cfr_u(T.row_cap) == 0) {
+    copy_row(T, s, src);
+    return;
+  }
+  const uint32_t* base = cfr_base(T);
+  CFR_SYNC();
+#if CIT_WAVE
+  {
+    const int l = CFR_LANE;
+    constexpr int NJ = (CFR_ROW_W + 63) / 64;
+    uint32_t v[NJ];
+    uint64_t m[NJ];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < NJ; j++) {
+      const int d = 64 * j + l;
+      v[j] = d < CFR_ROW_W ? src[d] : 0u;
+      m[j] = __ballot(d < CFR_ROW_W && v[j] != base[d]);
+      tot += (uint32_t)__popcll(m[j]);
+    }
+    if (tot > (uint32_t)cfr_u(T.row_cap)) {
+      T.err |= CIT_ERR_OVERFLOW;
+    } else {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < NJ; j++) {
+        if ((m[j] >> l) & 1) s[CFR_ROW_HDR + acc + cfr_mbcnt(m[j])] = v[j];
+        acc += (uint32_t)__popcll(m[j]);
+      }
+      uint32_t h = l == CFR_ROW_MASKW ? tot : 0u;
+#pragma unroll
+      for (int w = 0; w < CFR_ROW_MASKW; w++) h = l == w ? (uint32_t)(m[w >> 1] >> (32 * (w & 1))) : h;
+      if (l < CFR_ROW_HDR) s[l] = h;
+    }
+  }
+#else
+  {
+    uint32_t mask[CFR_ROW_MASKW] = {0};
+    uint32_t k = 0;
+    for (int d = 0; d < CFR_ROW_W; d++)
+      if (src[d] != base[d]) {
+        mask[d >> 5] |= 1u << (d & 31);
+        k++;
+      }
+    if (k > (uint32_t)T.row_cap) {
+      T.err |= CIT_ERR_OVERFLOW;
+    } else {
+      k = 0;
+      for (int d = 0; d < CFR_ROW_W; d++)
+        if ((mask[d >> 5] >> (d & 31)) & 1) s[CFR_ROW_HDR + k++] = src[d];
+      for (int w = 0; w < CFR_ROW_HDR; w++) s[w] = w < CFR_ROW_MASKW ? mask[w] : (w == CFR_ROW_MASKW ? k : 0u);
+    }
+  }
+#endif
+  CFR_SYNC();
+}
+// The tree's base row := working row src (its root game as first created), in
+// the pool and (device) in LDS.
+CIT_HD void row_set_base(CfrTree& T, const uint32_t* src) {
+  if (cfr_u(T.row_cap) == 0) return;
+  copy_row(T, cfr_glb(T.base_hbm), src);
+#if CIT_WAVE
+  copy_row(T, cfr_base_w(T), src);
+#endif
+}
+// A read-only view of node n's game: the slot itself for raw rows, else the
+// row decompressed into working row `which` (device) / the tree's scratch row.
+CIT_HD const CitGame& row_view(const CfrTree& T, int n, int which) {
+  if (cfr_u(T.row_cap) == 0) return *reinterpret_cast<const CitGame*>(row_of(T, n));
+#if CIT_WAVE
+  row_load(T, w_row(T, which), n);
+  return cfr_w(T, which);
+#else
+  (void)which;
+  row_load(T, T.scratch_hbm, n);
+  return *reinterpret_cast<const CitGame*>(T.scratch_hbm);
+#endif
 }
 
 // ------------------------------------------------------------ numpy fp64
@@ -612,7 +786,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   if ((id & (CFR_NB - 1)) == 0) {       // the first node of a new block
     int b = cfr_take_block(cfr_glb(T.arena), 0);
     if (b < 0) { T.err |= CIT_ERR_OVERFLOW; return -1; }
-    cfr_nbt(T)[id >> CFR_NB_SHIFT] = b;
+    cfr_nbt_at(T, id >> CFR_NB_SHIFT) = b;
   }
   T.n_nodes = id + 1;
   CfrNode& N = cfr_node(T, id);
@@ -644,7 +818,8 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   N.sib = -1;
   for (int k = 0; k < 6; k++) N.nv[k] = N.wp[k] = N.pred[k] = 0.0;
 #endif
-  copy_row(T, row_of(T, id), w_row(T, which));
+  if (id == 0) row_set_base(T, w_row(T, which));   // the root: the tree's base row
+  row_store(T, id, w_row(T, which));
   return id;
 }
 
@@ -656,7 +831,7 @@ CIT_HD int alloc_edges(CfrTree& T, int n) {
   while (((f + n - 1) >> CFR_EB_SHIFT) >= T.n_eblk) {
     int b = cfr_take_block(cfr_glb(T.arena), 1);
     if (b < 0) { T.err |= CIT_ERR_OVERFLOW; return -1; }
-    cfr_ebt(T)[T.n_eblk++] = b;
+    cfr_ebt_at(T, T.n_eblk++) = b;
   }
   T.n_edges = f + n;
   return f;
@@ -682,7 +857,7 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
   int depth = cfr_node(T, n).depth + 1;
   CitGame& h = cfr_w(T, 1);
   for (int r = 0; r < CFR_ROLE_CHILDREN && !T.err; r++) {
-    copy_row(T, w_row(T, 1), row_of(T, n));
+    row_load(T, w_row(T, 1), n);
     CitOpt last = mk(O_NUM_NAMES, 0);
     int guard = 0;
     while (h.gs_state != 1 && !T.err) {
@@ -710,13 +885,13 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
   CIT_PROF_SCOPE(9);                   // :133-151
   n = cfr_u(n);
   CitGame& g = cfr_w(T, 0);
-  copy_row(T, w_row(T, 0), row_of(T, n));
+  row_load(T, w_row(T, 0), n);
   eng_prepare(T, 0);
   CfrCnt lc = cfr_ucnt(eng_list(T, 0));
   int nl = lc.n;
   T.err |= lc.err | g.err;
   if (nl > CFR_OPT_CAP) T.err |= CIT_ERR_OVERFLOW;
-  copy_row(T, row_of(T, n), w_row(T, 0));   // get_options mutated the node's game
+  row_store(T, n, w_row(T, 0));   // get_options mutated the node's game
   if (T.err) return;
   int cnt = nl;
   int f = alloc_edges(T, cnt);
@@ -751,7 +926,7 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
   CIT_PROF_SCOPE(10);              // :153-179
   n = cfr_u(n);
   CfrNode& N = cfr_node(T, n);
-  copy_row(T, w_row(T, 1), row_of(T, n));
+  row_load(T, w_row(T, 1), n);
   CitGame& h = cfr_w(T, 1);
   int par = N.parent;
   if (par < 0 || N.player != cfr_node(T, par).player) eng_sample(T, 1, T.orig, par >= 0 && cfr_node(T, par).gs_state != 0);
@@ -887,7 +1062,7 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
   }
   const CfrWide* W = cfr_wide(T, N.first_edge);
   // weighted_average_strategy (:51-65) over turn_orders_for_roles of the node's game
-  const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
+  const CitGame& g = row_view(T, n, 1);
   if (nch > CFR_ROLE_CHILDREN) { T.err |= CIT_ERR_OVERFLOW; return -1; }
   double w[CFR_ROLE_CHILDREN];
   int hs = 0;
@@ -1069,7 +1244,7 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
     return (*cfr_edge(T, N.first_edge + a)).opt;
   }
   CitGame& g = cfr_w(T, 0);
-  copy_row(T, w_row(T, 0), row_of(T, root));
+  row_load(T, w_row(T, 0), root);
   eng_prepare(T, 0);
   CfrCnt lc = cfr_ucnt(eng_list(T, 0));
   int nl = lc.n;
@@ -1080,7 +1255,7 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
   double sum = 0.0;
   for (int j = 0; j < nl; j++) sum += W[ob[j].a].S[pid];
   int j = np_choice(T.np, [&](int i) { return W[ob[i].a].S[pid] / sum; }, nl, T.err);
-  copy_row(T, row_of(T, root), w_row(T, 0));
+  row_store(T, root, w_row(T, 0));
   if (T.err || j < 0) return mk(O_NUM_NAMES, 0);
   return ob[j];
 }
@@ -1112,10 +1287,15 @@ CIT_HD void cfr_state_save(const CfrTree& T, CfrState& S) {
 CIT_NOINLINE void cfr_write_feat(CfrTree& T_in, int n, float* feat) {
   CfrTree& T = CFR_T(T_in);
   n = cfr_u(n);
-  const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
   int pid = (cfr_node(T, n).flags & NF_ROLE_PICK) ? 5 : -1;
   CFR_SYNC();
-  cit_encode_game(g, cfr_glb(feat), pid);   // the whole team (identical stores): the engine's scans are wave-wide
+  // the whole team (identical stores): the engine's scans are wave-wide
+  if (cfr_u(T.row_cap) == 0) {
+    cit_encode_game(*reinterpret_cast<const CitGame*>(row_of(T, n)), cfr_glb(feat), pid);
+  } else {
+    row_load(T, w_row(T, 1), n);
+    cit_encode_game(cfr_w(T, 1), cfr_glb(feat), pid);
+  }
   CFR_SYNC();
 }
 
@@ -1277,7 +1457,7 @@ CIT_HD void cfr_emit_targets(const CfrTree& T, CitMT& py, int root, int mode, in
   for (int n = root; n >= 0; n = cfr_target_next(T, n, root, mode)) {
     if (!cfr_target_sel(T, n, mode)) continue;
     const CfrNode& N = cfr_node(T, n);
-    const CitGame& g = *reinterpret_cast<const CitGame*>(row_of(T, n));
+    const CitGame& g = row_view(T, n, 1);
     const CfrEdge* E = cfr_edge(T, N.first_edge);
     int pid = -1, row = 0;
     if (N.flags & NF_ROLE_PICK) {

@@ -45,8 +45,8 @@ __device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t
   CfrTree& T = cfr_ls.T;
   cfr_ls.cnode = -1;
   cfr_tree_bind(T, pool, B, l, node_cap, edge_cap);
-  T.nbt = cfr_ls.nbt;
-  T.ebt = cfr_ls.ebt;
+  T.nbt = nullptr;          // the tables live in dynamic LDS (cfr_nbt_at / cfr_ebt_at)
+  T.ebt = nullptr;
   T.n_eblk = 0;
   T.training = false;
   T.py = mt_stage_in(cfr_ls.py, mt, idx, B, l);
@@ -59,18 +59,21 @@ __device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t
   T.lbuf = cfr_ls.lbuf;
 }
 
-// The block tables of a tree between LDS and its pool (n node / e edge blocks).
+// The block tables (and, for diff row slots, the base row) of a resumed tree
+// from its pool into dynamic LDS (n node / e edge blocks), and the tables back.
 __device__ __forceinline__ void tables_load(const CfrTree& T, int n_nodes, int n_edges) {
   int nb = (n_nodes + CFR_NB - 1) >> CFR_NB_SHIFT, eb = (n_edges + CFR_EB - 1) >> CFR_EB_SHIFT;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) cfr_ls.nbt[i] = T.nbt_hbm[i];
-  for (int i = threadIdx.x; i < eb; i += blockDim.x) cfr_ls.ebt[i] = T.ebt_hbm[i];
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) cfr_nbt_at(T, i) = T.nbt_hbm[i];
+  for (int i = threadIdx.x; i < eb; i += blockDim.x) cfr_ebt_at(T, i) = T.ebt_hbm[i];
+  if (T.row_cap)
+    for (int i = threadIdx.x; i < CFR_ROW_W; i += blockDim.x) cfr_dyn[i] = T.base_hbm[i];
   __syncthreads();
 }
 __device__ __forceinline__ void tables_store(const CfrTree& T) {
   __syncthreads();
   int nb = (T.n_nodes + CFR_NB - 1) >> CFR_NB_SHIFT;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) T.nbt_hbm[i] = cfr_ls.nbt[i];
-  for (int i = threadIdx.x; i < T.n_eblk; i += blockDim.x) T.ebt_hbm[i] = cfr_ls.ebt[i];
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) T.nbt_hbm[i] = cfr_nbt_at(T, i);
+  for (int i = threadIdx.x; i < T.n_eblk; i += blockDim.x) T.ebt_hbm[i] = cfr_ebt_at(T, i);
 }
 
 // One MCCFR decision per workgroup: a 64-lane team runs the search on its
@@ -96,7 +99,7 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
   int root = cfr_train(T, iters, (flags & CIT_CFR_ROOT_SKIPPED) != 0);
   CitOpt c = mk(O_NUM_NAMES, 0);
   if (root >= 0 && !T.err) c = cfr_uopt(cfr_live_choice(T, root));
-  if (root >= 0) copy_row(T, games + l * ROW_W, row_of(T, root));
+  if (root >= 0) row_load(T, games + l * ROW_W, root);
   tables_store(T);
   mt_stage_out(cfr_ls.py, mt, B, l);
   mt_stage_out(cfr_ls.np, npmt, B, l);
@@ -148,7 +151,7 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
                        (flags & CIT_CFR_ROOT_SKIPPED) != 0);
   r = cfr_u(r);
   cfr_state_save(T, S);
-  if (!r && S.root >= 0) copy_row(T, games + l * ROW_W, row_of(T, S.root));
+  if (!r && S.root >= 0) row_load(T, games + l * ROW_W, S.root);
   tables_store(T);
   mt_stage_out(cfr_ls.py, mt, B, l);
   mt_stage_out(cfr_ls.np, npmt, B, l);
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(64) void k_cfr_train_slice(uint32_t* games, uint32_
   CitOpt c = mk(O_NUM_NAMES, 0);
   if (!r) {
     if (root >= 0 && !T.err) c = cfr_uopt(cfr_live_choice(T, root));
-    if (root >= 0) copy_row(T, games + l * ROW_W, row_of(T, root));
+    if (root >= 0) row_load(T, games + l * ROW_W, root);
   }
   cfr_state_save(T, S);
   tables_store(T);
@@ -249,11 +252,15 @@ __global__ void k_arena_release(int32_t* tables, long per_words, int nb, int eb,
 
 // A pool before its trees start: every block-table entry -1, the arena
 // header with no blocks handed out and the given capacities.
-__global__ void k_arena_reset(int32_t* tables, long n_words, CfrArena* a, uint32_t n_cap, uint32_t e_cap) {
+// Only the tables of each tree's region are set (its base / scratch rows are
+// written before they are read).
+__global__ void k_arena_reset(int32_t* pool, long per_words, long tbl_words, int B, CfrArena* a, uint32_t n_cap,
+                              uint32_t e_cap, uint32_t row_cap) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_words) tables[i] = -1;
+  if (i < tbl_words * B) pool[(i / tbl_words) * per_words + i % tbl_words] = -1;
   if (blockIdx.x == 0 && threadIdx.x < sizeof(CfrArena) / 4)
-    reinterpret_cast<uint32_t*>(a)[threadIdx.x] = threadIdx.x == 1 ? n_cap : threadIdx.x == 3 ? e_cap : 0u;
+    reinterpret_cast<uint32_t*>(a)[threadIdx.x] =
+        threadIdx.x == 1 ? n_cap : threadIdx.x == 3 ? e_cap : threadIdx.x == 8 ? row_cap : 0u;
 }
 
 }  // namespace
@@ -275,6 +282,10 @@ int64_t cit_cfr_arena_bytes(int node_blocks, int edge_blocks) {
   if (node_blocks < 0 || edge_blocks < 0) return -1;
   return cfr_arena_bytes(node_blocks, edge_blocks);
 }
+int64_t cit_cfr_arena_bytes_rows(int node_blocks, int edge_blocks, int row_cap) {
+  if (node_blocks < 0 || edge_blocks < 0 || !cfr_row_cap_ok(row_cap)) return -1;
+  return cfr_arena_bytes(node_blocks, edge_blocks, row_cap);
+}
 int cit_cfr_block_sizes(int32_t* out) {
   if (!out) return -1;
   out[0] = CFR_NB;
@@ -282,14 +293,23 @@ int cit_cfr_block_sizes(int32_t* out) {
   out[2] = CFR_TBL_MAX;
   return 0;
 }
+int cit_cfr_arena_reset_rows(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                             int row_cap, hipStream_t stream) {
+  if (!pool || B <= 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || node_blocks < 0 || edge_blocks < 0 ||
+      !cfr_row_cap_ok(row_cap))
+    return -1;
+  long per_words = (long)(cfr_pool_bytes(node_cap, edge_cap) / 4);
+  long tbl_words = (long)(cfr_tables_bytes(node_cap, edge_cap) / 4);
+  uint8_t* a = (uint8_t*)pool + per_words * 4 * B;
+  long n = tbl_words * B;
+  hipLaunchKernelGGL(k_arena_reset, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (int32_t*)pool,
+                     per_words, tbl_words, B, reinterpret_cast<CfrArena*>(a), (uint32_t)node_blocks,
+                     (uint32_t)edge_blocks, (uint32_t)row_cap);
+  CHECK_LAUNCH();
+}
 int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
                         hipStream_t stream) {
-  if (!pool || B <= 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || node_blocks < 0 || edge_blocks < 0) return -1;
-  long n_words = (long)(cfr_pool_bytes(node_cap, edge_cap) / 4) * B;
-  uint8_t* a = (uint8_t*)pool + n_words * 4;
-  hipLaunchKernelGGL(k_arena_reset, dim3((unsigned)((n_words + 255) / 256)), dim3(256), 0, stream, (int32_t*)pool,
-                     n_words, reinterpret_cast<CfrArena*>(a), (uint32_t)node_blocks, (uint32_t)edge_blocks);
-  CHECK_LAUNCH();
+  return cit_cfr_arena_reset_rows(pool, B, node_cap, edge_cap, node_blocks, edge_blocks, 0, stream);
 }
 int cit_cfr_arena_release(void* pool, int B, int node_cap, int edge_cap, const int32_t* lanes, int n_lanes,
                           hipStream_t stream) {
@@ -310,7 +330,7 @@ int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt,
   if (B <= 0 || iters < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt || !mt_idx || !np_mt ||
       !np_idx || !seer || !pool || !optbuf || !chosen || !stats)
     return -1;
-  hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
+  hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
                      B, iters, flags, orig_player, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats);
   CHECK_LAUNCH();
 }
@@ -324,7 +344,7 @@ int cit_cfr_train_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* n
   if (B <= 0 || iters < 0 || slice_ticks < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt ||
       !mt_idx || !np_mt || !np_idx || !seer || !pool || !optbuf || !state || !chosen || !stats || !running)
     return -1;
-  hipLaunchKernelGGL(k_cfr_train_slice, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
+  hipLaunchKernelGGL(k_cfr_train_slice, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
                      seer, B, iters, flags, orig_player, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
                      (CfrState*)state, (uint64_t)slice_ticks, (CitOpt*)chosen, stats, running);
   CHECK_LAUNCH();
@@ -337,7 +357,7 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
   if (B <= 0 || iters < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt || !mt_idx || !np_mt ||
       !np_idx || !seer || !pool || !optbuf || !state || !probs || !feat || !chosen || !waiting)
     return -1;
-  hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
+  hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
                      seer, B, iters, flags, orig_player, max_depth, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
                      (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting);
   CHECK_LAUNCH();

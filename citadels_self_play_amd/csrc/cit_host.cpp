@@ -147,13 +147,21 @@ void cith_advance_random(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer
 
 int64_t cith_cfr_pool_bytes(int node_cap, int edge_cap) { return cfr_pool_bytes(node_cap, edge_cap); }
 int64_t cith_cfr_arena_bytes(int node_blocks, int edge_blocks) { return cfr_arena_bytes(node_blocks, edge_blocks); }
-void cith_cfr_arena_reset(uint8_t* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks) {
+int64_t cith_cfr_arena_bytes_rows(int node_blocks, int edge_blocks, int row_cap) {
+  return cfr_row_cap_ok(row_cap) ? cfr_arena_bytes(node_blocks, edge_blocks, row_cap) : -1;
+}
+void cith_cfr_arena_reset_rows(uint8_t* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                               int row_cap) {
   int64_t tb = cfr_pool_bytes(node_cap, edge_cap) * (int64_t)B;
   memset(pool, 0xff, (size_t)tb);
   CfrArena* a = reinterpret_cast<CfrArena*>(pool + tb);
   memset(a, 0, sizeof(CfrArena));
   a->n_cap = (uint32_t)node_blocks;
   a->e_cap = (uint32_t)edge_blocks;
+  a->row_cap = (uint32_t)row_cap;
+}
+void cith_cfr_arena_reset(uint8_t* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks) {
+  cith_cfr_arena_reset_rows(pool, B, node_cap, edge_cap, node_blocks, edge_blocks, 0);
 }
 
 void cith_count_options(CitGame* g, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int* n_opts) {
@@ -225,7 +233,7 @@ void cith_cfr_decide(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, ui
     CitOpt c = mk(O_NUM_NAMES, 0);
     if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
     chosen[l] = c;
-    if (root >= 0) memcpy(&g[l], row_of(T, root), CIT_GAME_BYTES);
+    if (root >= 0) row_load(T, reinterpret_cast<uint32_t*>(&g[l]), root);
     idx[l] = T.py.pos;
     npidx[l] = T.np.pos;
     stats[5 * l + 0] = root;
@@ -286,7 +294,7 @@ int cith_cfr_train_slice(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt
     CitOpt c = mk(O_NUM_NAMES, 0);
     if (root >= 0 && !T.err) c = cfr_live_choice(T, root);
     chosen[l] = c;
-    if (root >= 0) memcpy(&g[l], row_of(T, root), CIT_GAME_BYTES);
+    if (root >= 0) row_load(T, reinterpret_cast<uint32_t*>(&g[l]), root);
     idx[l] = T.py.pos;
     npidx[l] = T.np.pos;
     stats[5 * l + 0] = root;
@@ -366,7 +374,7 @@ int cith_cfr_pred_step(CitGame* g, uint32_t* mt, uint32_t* idx, uint32_t* npmt, 
     waiting += r;
     if (!r) {
       chosen[l] = c;
-      if (S.root >= 0) memcpy(&g[l], row_of(T, S.root), CIT_GAME_BYTES);
+      if (S.root >= 0) row_load(T, reinterpret_cast<uint32_t*>(&g[l]), S.root);
     }
     idx[l] = T.py.pos;
     npidx[l] = T.np.pos;

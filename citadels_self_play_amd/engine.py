@@ -58,6 +58,19 @@ def pool_caps(iters):
     return node_cap, 4 * node_cap + 4096
 
 
+# Row slots of large trees' node pools: diffs against the tree's base row with
+# room for CFR_ROW_CAP differing dwords (cit_cfr.h; a cfr_train(200000) node
+# differs in ~70 of 388, at most ~100 measured): a node's pool bytes halve, so
+# twice the trees fit in HBM.  A tree with a row past the cap is searched again
+# with raw rows (_retry_overflow).  Small trees (configs 3/4) keep raw rows.
+CFR_ROW_CAP = 128
+ROW_CAP_MIN_BLOCKS = 16
+
+
+def row_cap_for(node_cap):
+    return CFR_ROW_CAP if L.cfr_nblocks(node_cap) >= ROW_CAP_MIN_BLOCKS else 0
+
+
 def arena_blocks(B, node_cap, edge_cap, frac=None):
     """Arena blocks (node, edge) for B trees: `frac` (a number, or a (node, edge)
     pair) of their worst case, at least one tree's worst case (None: all of it)."""
@@ -66,10 +79,11 @@ def arena_blocks(B, node_cap, edge_cap, frac=None):
     return (min(B * nbt, max(nbt, math.ceil(fn * B * nbt))), min(B * ebt, max(ebt, math.ceil(fe * B * ebt))))
 
 
-def pool_bytes(B, node_cap, edge_cap, frac=None):
-    """Device bytes of a B-tree node pool: block tables + arena (cit_cfr.h)."""
+def pool_bytes(B, node_cap, edge_cap, frac=None, row_cap="auto"):
+    """Device bytes of a B-tree node pool: per-tree regions + arena (cit_cfr.h)."""
     nb, eb = arena_blocks(B, node_cap, edge_cap, frac)
-    return B * L.cfr_pool_bytes(node_cap, edge_cap) + L.cfr_arena_bytes(nb, eb)
+    rc = row_cap_for(node_cap) if row_cap == "auto" else row_cap
+    return B * L.cfr_pool_bytes(node_cap, edge_cap) + L.cfr_arena_bytes(nb, eb, rc)
 
 
 def _ptr(t):
@@ -193,19 +207,18 @@ class GameBatch:
         over = ((stats[:, 4].to(self.device) & ERR_OVERFLOW) != 0).nonzero().flatten()
         if max_retries <= 0 or over.numel() == 0:
             return chosen, stats
-        # 4x caps when a lane reached its own node / edge cap; the same caps when
-        # only the shared arena ran out (the retry batch's arena holds every
-        # sub-tree's worst case, so a cap-limited lane misread as arena-limited
-        # still grows on its next retry)
+        # 4x caps when a lane reached its own node / edge cap, else the same caps
+        # (the retry batch's arena holds every sub-tree's worst case and raw
+        # rows, so a lane that overflowed for another reason cannot again)
+        # (arena out or a diff row past its slot: the same caps, raw rows)
         st = stats[over.to(stats.device)].cpu().numpy()
-        (n_used, e_used), (n_cap, e_cap) = self.arena_used()
-        arena_out = n_used > n_cap or e_used > e_cap
         cap_hit = bool(((st[:, 1] >= self.node_cap - 1) | (st[:, 2] + CFR_EDGE_SLACK >= self.edge_cap)).any())
-        grow = 4 if (cap_hit or not arena_out) else 1
+        grow = 4 if cap_hit else 1
         g, mt, idx, seer, npm, npi, steps = snap
         sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),
                                      seer[over].contiguous(), npm[:, over].contiguous(), npi[over].contiguous())
         sub.steps = steps[over].contiguous()
+        sub.row_cap = 0                           # a row past the diff-slot cap overflows too: raw rows
         sub_orig = None if orig is None else \
             np.broadcast_to(np.asarray(orig, np.int32), (self.B,))[over.cpu().numpy()].copy()
         nc = min(grow * self.node_cap, L.CFR_TBL_MAX * L.CFR_NB)
@@ -353,6 +366,7 @@ class GameBatch:
         return out
 
     arena_frac = None       # arena blocks as a fraction of the trees' worst case (arena_blocks)
+    row_cap = "auto"        # row slot format: 0 raw rows, K diff rows (row_cap_for by node_cap)
 
     def _pool(self, node_cap, edge_cap):
         """Node pool for B trees of (node_cap, edge_cap): block tables + an arena
@@ -365,7 +379,8 @@ class GameBatch:
         if per <= 0 or node_cap >= 2 ** 31 or edge_cap >= 2 ** 31:
             raise ValueError("bad node pool capacity (%d nodes, %d edges)" % (node_cap, edge_cap))
         nb, eb = arena_blocks(self.B, node_cap, edge_cap, self.arena_frac)
-        need = per * self.B + self.lib.cit_cfr_arena_bytes(nb, eb)
+        rc = row_cap_for(node_cap) if self.row_cap == "auto" else int(self.row_cap)
+        need = per * self.B + self.lib.cit_cfr_arena_bytes_rows(nb, eb, rc)
         have = self.pool.numel() if getattr(self, "pool", None) is not None else 0
         if need > have and self.device.type == "cuda":
             avail = int(0.9 * (torch.cuda.mem_get_info(self.device)[0] + have))
@@ -374,7 +389,7 @@ class GameBatch:
                 scale = max(0.0, (avail - per * self.B) / float(need - per * self.B))
                 nb0, eb0 = nb, eb
                 nb, eb = max(nbt, int(nb * scale)), max(ebt, int(eb * scale))
-                need = per * self.B + self.lib.cit_cfr_arena_bytes(nb, eb)
+                need = per * self.B + self.lib.cit_cfr_arena_bytes_rows(nb, eb, rc)
                 warnings.warn("node arena cut to %.0f%% of the requested %d node / %d edge blocks (%d trees): "
                               "device memory is short, trees that find it exhausted are searched again "
                               "(slower, same results); use fewer trees per batch to avoid this"
@@ -386,9 +401,9 @@ class GameBatch:
             self.pool = torch.empty(need, dtype=torch.uint8, device=self.device)
         if getattr(self, "optbuf", None) is None or self.optbuf.shape[0] != self.B:
             self.optbuf = torch.empty((self.B, self.lib.cit_cfr_opt_cap(), 16), dtype=torch.uint8, device=self.device)
-        self.node_cap, self.edge_cap, self.arena = node_cap, edge_cap, (nb, eb)
-        _lib.check(self.lib.cit_cfr_arena_reset(_ptr(self.pool), self.B, node_cap, edge_cap, nb, eb, _stream()),
-                   "cit_cfr_arena_reset")
+        self.node_cap, self.edge_cap, self.arena, self.pool_row_cap = node_cap, edge_cap, (nb, eb), rc
+        _lib.check(self.lib.cit_cfr_arena_reset_rows(_ptr(self.pool), self.B, node_cap, edge_cap, nb, eb, rc,
+                                                     _stream()), "cit_cfr_arena_reset_rows")
 
     def train_slice(self, iters, state, ticks, chosen, stats, running, flags=0):
         """One cit_cfr_train_slice launch over the pool bound by _pool (state [B,16]

@@ -79,12 +79,15 @@ def opt_from_bytes(b):
     return CitOpt.from_buffer_copy(bytes(b)[:16])
 
 
-# ---- MCCFR node pools (csrc/cit_cfr.h): B per-tree block tables, then one arena
-# of node blocks (CFR_NB node records + CFR_NB game rows) and edge blocks
-# (CFR_EB edge slots) the trees take as they grow.  tests/test_abi.py checks
+# ---- MCCFR node pools (csrc/cit_cfr.h): B per-tree regions (block tables, base
+# row, scratch row), then one arena of node blocks (CFR_NB node records +
+# CFR_NB row slots) and edge blocks (CFR_EB edge slots) the trees take as they
+# grow.  Row slots are raw game rows (row_cap 0) or diffs against the tree's
+# base row holding at most row_cap differing dwords.  tests/test_abi.py checks
 # these constants against the library (cit_cfr_block_sizes / cit_cfr_sizes).
 CFR_NB, CFR_EB, CFR_TBL_MAX = 4096, 16384, 1024
 CFR_NODE_BYTES, CFR_EDGE_BYTES, CFR_ARENA_HDR = 168, 48, 64
+CFR_ROW_W, CFR_ROW_HDR, CFR_ROW_MASKW, CFR_ROW_CAP_MAX = GAME_BYTES // 4, 16, 13, 368
 
 
 def cfr_nblocks(node_cap):
@@ -95,13 +98,22 @@ def cfr_eblocks(edge_cap):
     return -(-int(edge_cap) // CFR_EB)
 
 
-def cfr_pool_bytes(node_cap, edge_cap):
-    """Bytes per tree ahead of the arena: its node- and edge-block tables (int32, -1 = none)."""
+def cfr_tables_bytes(node_cap, edge_cap):
+    """A tree's node- and edge-block tables (int32, -1 = none), padded to 16 B."""
     return (4 * (cfr_nblocks(node_cap) + cfr_eblocks(edge_cap)) + 15) // 16 * 16
 
 
-def cfr_node_block_bytes():
-    return CFR_NB * (CFR_NODE_BYTES + GAME_BYTES)
+def cfr_pool_bytes(node_cap, edge_cap):
+    """Bytes per tree ahead of the arena: its tables, base row and scratch row."""
+    return cfr_tables_bytes(node_cap, edge_cap) + 2 * GAME_BYTES
+
+
+def cfr_row_slot_bytes(row_cap=0):
+    return 4 * (CFR_ROW_HDR + row_cap) if row_cap else GAME_BYTES
+
+
+def cfr_node_block_bytes(row_cap=0):
+    return CFR_NB * (CFR_NODE_BYTES + cfr_row_slot_bytes(row_cap))
 
 
 def cfr_ring_bytes(n_blocks, e_blocks):
@@ -109,9 +121,19 @@ def cfr_ring_bytes(n_blocks, e_blocks):
     return (4 * (n_blocks + e_blocks) + 15) // 16 * 16
 
 
-def cfr_arena_bytes(n_blocks, e_blocks):
-    return CFR_ARENA_HDR + cfr_ring_bytes(n_blocks, e_blocks) + n_blocks * cfr_node_block_bytes() + \
+def cfr_arena_bytes(n_blocks, e_blocks, row_cap=0):
+    return CFR_ARENA_HDR + cfr_ring_bytes(n_blocks, e_blocks) + n_blocks * cfr_node_block_bytes(row_cap) + \
         e_blocks * CFR_EB * CFR_EDGE_BYTES
+
+
+def cfr_row_decode(slot, base):
+    """A diff row slot (uint8 [slot bytes]) against the tree's base row -> the game row."""
+    import numpy as np
+    w = np.asarray(slot).view("<u4")
+    mask = np.unpackbits(w[:CFR_ROW_MASKW].view(np.uint8), bitorder="little")[:CFR_ROW_W].astype(bool)
+    out = np.array(np.asarray(base).view("<u4"), copy=True)
+    out[mask] = w[CFR_ROW_HDR:CFR_ROW_HDR + int(mask.sum())]
+    return out.view(np.uint8)
 
 
 def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
@@ -122,11 +144,12 @@ def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
     per = cfr_pool_bytes(node_cap, edge_cap)
     nb, eb = cfr_nblocks(node_cap), cfr_eblocks(edge_cap)
     tbl = np.array(read(lane * per, 4 * (nb + eb))).view("<i4")
-    hdr = np.array(read(B * per, 16)).view("<u4")
-    n_cap, e_cap = int(hdr[1]), int(hdr[3])
+    hdr = np.array(read(B * per, 48)).view("<u4")
+    n_cap, e_cap, row_cap = int(hdr[1]), int(hdr[3]), int(hdr[8])
+    slot = cfr_row_slot_bytes(row_cap)
     node_base = B * per + CFR_ARENA_HDR + cfr_ring_bytes(n_cap, e_cap)
     row_base = node_base + n_cap * CFR_NB * CFR_NODE_BYTES
-    edge_base = row_base + n_cap * CFR_NB * GAME_BYTES
+    edge_base = row_base + n_cap * CFR_NB * slot
 
     def held(t):
         out = []
@@ -142,6 +165,14 @@ def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
 
     nbl, ebl = held(tbl[:nb]), held(tbl[nb:])
     nodes = gather(node_base, CFR_NB * CFR_NODE_BYTES, nbl)
-    rows = gather(row_base, CFR_NB * GAME_BYTES, nbl).reshape(-1, GAME_BYTES)
+    rows = gather(row_base, CFR_NB * slot, nbl).reshape(-1, slot)
+    if row_cap:
+        base = np.array(read(lane * per + cfr_tables_bytes(node_cap, edge_cap), GAME_BYTES)).view("<u4")
+        w = np.ascontiguousarray(rows).view("<u4")
+        bits = np.unpackbits(np.ascontiguousarray(w[:, :CFR_ROW_MASKW]).view(np.uint8), axis=1,
+                             bitorder="little")[:, :CFR_ROW_W].astype(bool)
+        rank = np.clip(np.cumsum(bits, axis=1) - 1, 0, row_cap - 1) + CFR_ROW_HDR
+        vals = np.take_along_axis(w, rank, axis=1)
+        rows = np.where(bits, vals, base[None, :]).astype("<u4").view(np.uint8)   # unused slots decode to garbage
     edges = gather(edge_base, CFR_EB * CFR_EDGE_BYTES, ebl)
     return nodes, edges, rows

@@ -48,7 +48,7 @@ typedef struct CitOption {
   uint64_t x;
 } CitOption;
 
-int cit_abi_version(void);              /* 3: block-allocated node pools (cit_cfr_arena_reset) */
+int cit_abi_version(void);              /* 4: node pools with diff row slots (cit_cfr_arena_reset_rows) */
 int cit_game_bytes(void);              /* row width of `games` */
 int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
 int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
@@ -138,12 +138,18 @@ int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1,
 
 /* --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------ */
 
-/* Node pools.  A pool of B trees = B per-tree block tables
- * (cit_cfr_pool_bytes each: int32 node-block and edge-block tables for
- * node_cap / edge_cap) followed by one arena (cit_cfr_arena_bytes(node_blocks,
- * edge_blocks)): a 64-byte header, node blocks (CFR_NB CfrNode records of
- * 168 B + CFR_NB packed game rows, 16-byte aligned) and edge blocks (CFR_EB
- * CfrEdge slots of 48 B), after a ring of free block ids per kind.  A
+/* Node pools.  A pool of B trees = B per-tree regions (cit_cfr_pool_bytes
+ * each: int32 node-block and edge-block tables for node_cap / edge_cap,
+ * padded to 16 B, then the tree's base row and a scratch row) followed by one
+ * arena (cit_cfr_arena_bytes_rows(node_blocks, edge_blocks, row_cap)): a
+ * 64-byte header, node blocks (CFR_NB CfrNode records of 168 B + CFR_NB row
+ * slots, 16-byte aligned) and edge blocks (CFR_EB CfrEdge slots of 48 B),
+ * after a ring of free block ids per kind.  A row slot holds a node's packed
+ * game row raw (row_cap 0: CIT_GAME_BYTES) or as a diff against the tree's
+ * base row (its root game as first created): 16 header words (a 388-bit mask
+ * of the differing dwords, their count) + at most row_cap dwords (a multiple
+ * of 4, <= 368); a row with more differing dwords stops the tree with
+ * CIT_ERR_OVERFLOW (search it again with raw rows).  A
  * tree takes blocks as it grows (a released block first), so the arena holds
  * what the trees use, not B worst cases; a tree that reaches its own caps or
  * finds the arena exhausted stops with CIT_ERR_OVERFLOW (search it again with
@@ -152,13 +158,17 @@ int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1,
  * straddle an edge block.  Sizes are 64-bit; -1 on a bad capacity (either
  * table longer than out[2] of cit_cfr_block_sizes). */
 int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap);
-int64_t cit_cfr_arena_bytes(int node_blocks, int edge_blocks);
+int64_t cit_cfr_arena_bytes_rows(int node_blocks, int edge_blocks, int row_cap);
+int64_t cit_cfr_arena_bytes(int node_blocks, int edge_blocks);     /* = ..._rows(.., 0): raw rows */
 /* out[3] = {CFR_NB nodes per node block, CFR_EB edges per edge block,
  * table entries a tree may hold}. */
 int cit_cfr_block_sizes(int32_t* out);
 /* Before a search (cit_cfr_decide, or the first cit_cfr_pred_step): every
- * table entry -1 and the arena empty with node_blocks / edge_blocks capacity.
- * pool must hold B * cit_cfr_pool_bytes + cit_cfr_arena_bytes(...) bytes. */
+ * table entry -1 and the arena empty with node_blocks / edge_blocks capacity
+ * and row slots of row_cap.  pool must hold B * cit_cfr_pool_bytes +
+ * cit_cfr_arena_bytes_rows(...) bytes.  cit_cfr_arena_reset = row_cap 0. */
+int cit_cfr_arena_reset_rows(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                             int row_cap, hipStream_t stream);
 int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
                         hipStream_t stream);
 int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */

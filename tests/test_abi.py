@@ -32,7 +32,7 @@ def test_layout_matches(lib):
     assert list(out[:n]) == L.expected_layout()
     assert lib.cit_game_bytes() == L.GAME_BYTES
     assert lib.cit_seer_scratch_words() == L.SEER_MAX
-    assert lib.cit_abi_version() == 3
+    assert lib.cit_abi_version() == 4
 
 
 def test_cfr_pool_layout(lib):
@@ -45,9 +45,18 @@ def test_cfr_pool_layout(lib):
     assert h.cith_cfr_sizes(out) == 5
     assert list(out[:5]) == [L.CFR_NODE_BYTES, L.CFR_EDGE_BYTES, lib.cit_cfr_opt_cap(), L.CFR_NB, L.CFR_EB]
     nc, ec = 700_512, 4 * 700_512 + 4096                      # pool_caps(200000)
-    assert lib.cit_cfr_pool_bytes(nc, ec) == L.cfr_pool_bytes(nc, ec) == (4 * (172 + 172) + 15) // 16 * 16
+    # per tree: tables, then its base row and a scratch row
+    assert lib.cit_cfr_pool_bytes(nc, ec) == L.cfr_pool_bytes(nc, ec) == (4 * (172 + 172) + 15) // 16 * 16 + 2 * 1552
     assert lib.cit_cfr_pool_bytes(3, 5) % 16 == 0             # the next tree's tables 16-byte aligned
     assert lib.cit_cfr_arena_bytes(172 * 300, 172 * 300) == L.cfr_arena_bytes(172 * 300, 172 * 300) > 2 ** 38
+    h.cith_cfr_arena_bytes_rows.restype = C.c_int64
+    for rc in (0, 4, 128, 368):                               # diff row slots: 16 header words + rc dwords
+        assert lib.cit_cfr_arena_bytes_rows(172, 17, rc) == L.cfr_arena_bytes(172, 17, rc) == \
+            h.cith_cfr_arena_bytes_rows(172, 17, rc)
+    assert L.cfr_node_block_bytes(128) == 4096 * (168 + 576) < L.cfr_node_block_bytes(0) == 4096 * (168 + 1552)
+    for bad in (-4, 3, 130, 372):
+        assert lib.cit_cfr_arena_bytes_rows(1, 1, bad) == -1
+        assert lib.cit_cfr_arena_reset_rows(None, 4, 16, 16, 1, 1, bad, None) == -1
     assert lib.cit_cfr_pool_bytes(0, 10) == -1
     assert lib.cit_cfr_pool_bytes(L.CFR_TBL_MAX * L.CFR_NB + 1, 10) == -1   # table longer than a tree may hold
     assert lib.cit_cfr_arena_bytes(-1, 0) == -1
@@ -59,7 +68,9 @@ def test_arena_blocks():
     assert arena_blocks(10, 700_512, 2_806_144) == (1720, 1720)
     assert arena_blocks(10, 700_512, 2_806_144, (0.5, 0.8)) == (860, 1376)
     assert arena_blocks(1, 100, 500, 0.1) == (1, 1)           # never below one tree's worst case
-    assert pool_bytes(2, 100, 500) == 2 * 16 + L.cfr_arena_bytes(2, 2)
+    assert pool_bytes(2, 100, 500) == 2 * (16 + 2 * 1552) + L.cfr_arena_bytes(2, 2)
+    assert pool_bytes(2, 700_512, 2_806_144) == 2 * L.cfr_pool_bytes(700_512, 2_806_144) + \
+        L.cfr_arena_bytes(344, 344, 128)                       # large trees: diff row slots
 
 
 def test_bad_args_rejected(lib):

@@ -134,3 +134,43 @@ def test_gpu_pool_overflow_retry():
         for x, y in zip(a, bb):
             for u, v in zip(x, y):
                 assert np.array_equal(u, v)
+
+
+@pytest.mark.parametrize("row_cap", [128, 8])
+def test_gpu_diff_rows_match_raw_rows(row_cap):
+    """Node rows stored as diffs against the tree's base row (the default for
+    large trees, engine.row_cap_for) give the trees, decisions, streams and
+    targets of raw rows; with a cap too small for any row (8 dwords) every
+    tree overflows and is searched again with raw rows, same results."""
+    from citadels_self_play_amd.engine import GameBatch
+    seeds = np.arange(7_200_000, 7_200_048)
+    out = []
+    for rc in (0, row_cap):
+        b = GameBatch(seeds, preset=True)
+        b.random_position(100)
+        b.seed_numpy()
+        b.row_cap = rc
+        chosen, stats = b.cfr_decide(2000, node_cap=8192, edge_cap=8 * 8192)
+        t = b.cfr_targets(stats[:, 0])
+        torch.cuda.synchronize()
+        trees = [b.tree(l) for l in (0, 7, 31)]
+        out.append((chosen.cpu().numpy(), stats.cpu().numpy(), _split(t), b.rows(), b.mt.cpu().numpy(),
+                    b.np_mt.cpu().numpy(), trees, getattr(b, "_retry", None) is not None))
+    raw, diff = out
+    assert diff[7] == (row_cap == 8)                  # the tiny cap overflowed every tree into the retry
+    for x, y in zip(raw[:2] + raw[3:6], diff[:2] + diff[3:6]):
+        assert np.array_equal(x, y)
+    for a, bb in zip(raw[2], diff[2]):
+        assert len(a) == len(bb)
+        for x, y in zip(a, bb):
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v)
+    for l, (n0, e0, r0), (n1, e1, r1) in zip((0, 7, 31), raw[6], diff[6]):
+        n = int(raw[1][l, 1])
+        assert np.array_equal(n0[:n], n1[:n])
+        assert np.array_equal(r0[:n], r1[:n])               # every node's game row, decoded
+        # the written edge slots (reserved ones that were never filled hold garbage)
+        f, c, rp = n0["first_edge"][:n], n0["n_children"][:n], (n0["flags"][:n] & 1) != 0
+        idx = np.concatenate([np.arange(a, a + (40 if r else k)) for a, k, r in zip(f, c, rp) if k > 0])
+        ed = idx[~np.isin(idx, np.concatenate([np.arange(a + k, a + 10) for a, k, r in zip(f, c, rp) if r]))]
+        assert np.array_equal(e0[ed], e1[ed])

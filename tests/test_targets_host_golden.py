@@ -14,14 +14,14 @@ from test_cfr_host_golden import hash_obj
 from test_targets_oracle_golden import check_targets
 
 
-@pytest.mark.parametrize("mode", [0, 2])      # 2: the pruned walk (trees searched without a model)
-def test_host_targets_match_reference(mode):
+@pytest.mark.parametrize("mode,row_cap", [(0, 0), (2, 0), (2, 128)])   # 2: the pruned walk (no model);
+def test_host_targets_match_reference(mode, row_cap):                    # 128: diff row slots
     recs = load_golden("targets2000.json.gz")
     hb = HostBatch([r["seed"] for r in recs], True)
     random_position(hb, 100)
     for l, r in enumerate(recs):
         assert canon.canon_game(hb.game(l)) == r["position"], r["seed"]
-    cf = HostCfr(hb, node_cap=8192, edge_cap=8 * 8192)
+    cf = HostCfr(hb, node_cap=8192, edge_cap=8 * 8192, row_cap=row_cap)
     chosen, stats = cf.decide(2000)
     t = cfr_targets(cf, stats[:, 0], mode=mode)
     per = split_targets(t)

@@ -481,7 +481,9 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
     iters = {3: 200, 4: 200, 5: args.cfg5_iters}[config]
     per_gpu = {3: 1024, 4: max(1, 4096 // world), 5: args.cfg5_trees}[config]
     net = _value_net(dev) if config == 4 else None
-    node_cap = {3: 1024, 4: 2048}.get(config)
+    # one 4096-node block per tree either way; room enough that no config-3/4 tree
+    # overflows into the (serial) retry
+    node_cap = {3: 4096, 4: 4096}.get(config)
     reps = []
     stream = torch.cuda.current_stream()
     n_reps = args.cfg5_reps if config == 5 else args.cfr_reps

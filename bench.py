@@ -55,6 +55,9 @@ Prints ONE JSON line on rank 0.  `value` = carry_out transitions of all ranks
        (default 200000, the reference's own setting) through the tree queue,
        targets pooled with the RCCL all-gather
   At N = 1, config 3 also carries in-run PMC passes of its search kernel.
+  Config 3's `value` runs consecutive batches on --cfr-streams HIP streams
+  (a continuous self-play loop, as config 2); `value_one_batch` is one batch
+  at a time.
 * `--config 3|4|5` makes that config the headline line instead (used for the
   PMC children and for A/B runs).
 """
@@ -218,8 +221,8 @@ def _pmc_pass(counters, outdir, config=2, timeout_s=150):
     os.makedirs(outdir, exist_ok=True)
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(config), "--no-cpu-baseline", "--no-pmc",
              "--no-cfr"]
-    child += ["--steps", "2", "--warmup", "1", "--streams", "1"] if config == 2 else ["--cfr-reps", "1", "--cfg5-reps",
-                                                                                      "1"]
+    child += ["--steps", "2", "--warmup", "1", "--streams", "1"] if config == 2 else [
+        "--cfr-reps", "1", "--cfg5-reps", "1", "--cfr-streams", "1"]
     cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", outdir, "-o", "run", "--"] + child
     env = dict(os.environ, TMPDIR="/tmp")
     with open(os.path.join(outdir, "log.txt"), "w") as log:
@@ -509,7 +512,8 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
             chosen, stats, rounds = b.cfr_pred(it, net, max_depth=10, node_cap=node_cap)
             term = b.terminal()
         else:
-            b, stats, t = selfplay.simulate_games(seeds, it)
+            b, stats, t = selfplay.simulate_games(
+                seeds, it, log=(lambda m: print(m, file=sys.stderr, flush=True)) if (rank == 0 and not warm) else None)
             f, v = selfplay.all_gather_targets(t["feat"], t["value"])
             n_targets = int(f.shape[0])
             term = t["terminal"]
@@ -527,6 +531,9 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
                      "value": units / el_max, "carry_out_per_s": carry / el_max, "nodes": nodes, "edges": edges,
                      "error_lanes_nonterminal": int(errs), "terminal_positions": int(terms), "leaf_rounds": rounds,
                      "pooled_targets": n_targets})
+    streams = None
+    if config == 3 and args.cfr_streams > 1:
+        streams = _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap)
     if rank != 0:
         return None
     med = sorted(reps, key=lambda r: r["value"])[len(reps) // 2]
@@ -542,7 +549,8 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
            "leaves (torch.manual_seed(0) weights)" % per_gpu,
         5: "config5: %d simulate_game trees per GPU: create_a_random_game(100) -> cfr_train(%d) -> "
            "get_all_targets(200), tree queue, targets all-gathered" % (per_gpu, iters)}[config],
-        "value": med["value"], "unit": "trees/s" if config == 5 else "decisions/s",
+        "value": streams["value"] if streams else med["value"], "unit": "trees/s" if config == 5 else "decisions/s",
+        "value_one_batch": med["value"], "streams": streams,
         "carry_out_per_s": med["carry_out_per_s"], "reps": len(reps), "median": med,
         "all_reps_value": [r["value"] for r in reps],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -574,6 +582,47 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
     return out
 
 
+def _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap):
+    """Config 3 as a continuous self-play loop: K consecutive batches of
+    `per_gpu` positions (built untimed) whose searches are launched
+    round-robin on S HIP streams, so the next batch's trees take the SIMD
+    slots the finished trees of earlier batches free (a launch lasts as long
+    as its longest tree).  Decisions of all ranks / max-over-ranks time."""
+    from citadels_self_play_amd import selfplay
+    from citadels_self_play_amd.engine import ERR_OVERFLOW, GameBatch
+    K, S = args.cfr_stream_batches, args.cfr_streams
+    batches = []
+    for k in range(K + S):
+        seeds = selfplay.shard(per_gpu * world, base_seed=CFR_SEED + 50_000_000 + k * 1_000_000)
+        b = GameBatch(seeds, preset=True, device=dev)
+        b.advance_random(0, 300)
+        b.seed_numpy()
+        b._pool(node_cap, 5 * node_cap)
+        batches.append(b)
+    torch.cuda.synchronize()
+    sts = [torch.cuda.Stream(device=dev) for _ in range(S)]
+    for i, st in enumerate(sts):                       # warm each stream's queue (untimed batches)
+        with torch.cuda.stream(st):
+            batches[K + i]._cfr_decide(iters, node_cap, 5 * node_cap)
+    torch.cuda.synchronize()
+    out = []
+    _barrier(world)
+    t0 = time.perf_counter()
+    for k, b in enumerate(batches[:K]):
+        with torch.cuda.stream(sts[k % S]):
+            out.append(b._cfr_decide(iters, node_cap, 5 * node_cap)[1])
+    torch.cuda.synchronize()
+    _barrier(world)
+    el = time.perf_counter() - t0
+    st = torch.cat(out).to(torch.float64)
+    over = int(((torch.cat(out)[:, 4] & ERR_OVERFLOW) != 0).sum())
+    el, units, carry, over = _reduce([el, st.shape[0], st[:, 3].sum(), over], world, dev, maxes=(0,))
+    return {"value": units / el, "carry_out_per_s": carry / el, "batches": K, "streams": S, "seconds": el,
+            "overflow_lanes": int(over),
+            "note": "K batches of positions searched round-robin on S HIP streams (untimed position setup); "
+                    "value_one_batch is the median of one batch at a time"}
+
+
 def _cpu_model():
     from citadels_self_play_amd import models
     torch.manual_seed(0)
@@ -600,7 +649,9 @@ def main():
     ap.add_argument("--cfr-reps", type=int, default=5, help="timed reps of configs 3 and 4 (median reported)")
     ap.add_argument("--cfg5-reps", type=int, default=1, help="timed reps of config 5")
     ap.add_argument("--cfr-cpu-seconds", type=float, default=4.0, help="per C++ CPU-baseline leg of configs 3-5")
-    ap.add_argument("--cfg5-trees", type=int, default=640, help="config 5 trees per GPU")
+    ap.add_argument("--cfr-streams", type=int, default=2, help="config 3: HIP streams for consecutive batches")
+    ap.add_argument("--cfr-stream-batches", type=int, default=8, help="config 3: batches in the streams run")
+    ap.add_argument("--cfg5-trees", type=int, default=1920, help="config 5 trees per GPU")
     ap.add_argument("--cfg5-iters", type=int, default=200000, help="config 5 cfr_train iterations per tree")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the real path); gloo only to rehearse N>1 ranks on one GPU")

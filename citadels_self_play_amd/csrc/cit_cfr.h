@@ -510,7 +510,7 @@ CIT_HD void row_store(CfrTree& T, int id, const uint32_t* src) {
       tot += (uint32_t)__popcll(m[j]);
     }
     if (tot > (uint32_t)cfr_u(T.row_cap)) {
-      T.err |= CIT_ERR_OVERFLOW;
+      T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_ROW;
     } else {
       uint32_t acc = 0;
 #pragma unroll
@@ -534,7 +534,7 @@ CIT_HD void row_store(CfrTree& T, int id, const uint32_t* src) {
         k++;
       }
     if (k > (uint32_t)T.row_cap) {
-      T.err |= CIT_ERR_OVERFLOW;
+      T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_ROW;
     } else {
       k = 0;
       for (int d = 0; d < CFR_ROW_W; d++)
@@ -781,11 +781,11 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
     if (i > 100) done = true;
   }
   T.err |= e | w.err;
-  if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+  if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_CAP; return -1; }
   int id = T.n_nodes;
   if ((id & (CFR_NB - 1)) == 0) {       // the first node of a new block
     int b = cfr_take_block(cfr_glb(T.arena), 0);
-    if (b < 0) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+    if (b < 0) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_ARENA; return -1; }
     cfr_nbt_at(T, id >> CFR_NB_SHIFT) = b;
   }
   T.n_nodes = id + 1;
@@ -827,10 +827,10 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
 CIT_HD int alloc_edges(CfrTree& T, int n) {
   int f = T.n_edges;
   if ((f & (CFR_EB - 1)) + n > CFR_EB) f = (f | (CFR_EB - 1)) + 1;
-  if (f + n > T.edge_cap) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+  if (f + n > T.edge_cap) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_CAP; return -1; }
   while (((f + n - 1) >> CFR_EB_SHIFT) >= T.n_eblk) {
     int b = cfr_take_block(cfr_glb(T.arena), 1);
-    if (b < 0) { T.err |= CIT_ERR_OVERFLOW; return -1; }
+    if (b < 0) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_ARENA; return -1; }
     cfr_ebt_at(T, T.n_eblk++) = b;
   }
   T.n_edges = f + n;

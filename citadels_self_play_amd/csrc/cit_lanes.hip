@@ -72,6 +72,10 @@ __global__ void k_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_
                                    int32_t* counts) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= B) return;
+  if (roots[l] < 0) {
+    counts[2 * l] = counts[2 * l + 1] = 0;
+    return;
+  }
   CfrTree T = cfr_tree_view(pool, B, l, node_cap, edge_cap);
   cfr_count_targets(T, roots[l], mode, counts[2 * l], counts[2 * l + 1]);
 }
@@ -81,7 +85,9 @@ __global__ void k_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, 
                               uint32_t* idx, const int32_t* offsets, int32_t* meta, float* feat, double* value,
                               double* dist, float* opt_feat) {
   long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= B) return;
+  // a lane without a tree touches nothing: the tree queue walks finished trees while
+  // the other lanes' searches run (and write their own stream positions) on another stream
+  if (l >= B || roots[l] < 0) return;
   CfrTree T = cfr_tree_view(pool, B, l, node_cap, edge_cap);
   CitMT r = lane_mt(mt, idx, B, l);
   cfr_emit_targets(T, r, roots[l], mode, (int)l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);

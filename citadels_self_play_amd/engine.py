@@ -11,6 +11,7 @@ PyTorch supplies device memory and the stream; the compute is the native
 library.  Every call is asynchronous on torch's current stream.
 """
 import math
+import os
 import warnings
 
 import numpy as np
@@ -25,13 +26,14 @@ NODE_DT = np.dtype([("parent", "<i4"), ("first_edge", "<i4"), ("n_children", "<i
                     ("depth", "<i2"), ("player", "i1"), ("gs_state", "i1"), ("flags", "u1"), ("winner", "i1"),
                     ("sib", "<i2"), ("pad", "u1", 4), ("nv", "<f8", 6), ("wp", "<f8", 6), ("pred", "<f8", 6)])
 ERR_OVERFLOW = 0x1         # CIT_ERR_OVERFLOW (csrc/cit_core.h)
+# With ERR_OVERFLOW: which node-pool capacity ran out (CIT_ERR_POOL_*); only
+# these are searched again (an overflow without them is an engine list
+# capacity no retry fixes)
+ERR_POOL_ARENA, ERR_POOL_CAP, ERR_POOL_ROW = 0x1000, 0x2000, 0x4000
+ERR_POOL = ERR_POOL_ARENA | ERR_POOL_CAP | ERR_POOL_ROW
 EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8"), ("S", "<f8"), ("CS", "<f8")])
 WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])   # role-pick columns (csrc/cit_cfr.h)
 CFR_ROOT_SKIPPED = 1       # CIT_CFR_ROOT_SKIPPED (include/citadels.h)
-# Edge slots a node creation may reserve at once (a role-pick node: 10 edges +
-# 10 three-slot CfrWide records, csrc/cit_cfr.h): an overflowing tree within
-# this of its edge cap counts as cap-limited.
-CFR_EDGE_SLACK = 64
 
 
 def node_arrays(nodes, edges, n):
@@ -63,7 +65,7 @@ def pool_caps(iters):
 # differs in ~70 of 388, at most ~100 measured): a node's pool bytes halve, so
 # twice the trees fit in HBM.  A tree with a row past the cap is searched again
 # with raw rows (_retry_overflow).  Small trees (configs 3/4) keep raw rows.
-CFR_ROW_CAP = 128
+CFR_ROW_CAP = int(os.environ.get("CIT_ROW_CAP", "128"))      # (0: raw rows everywhere, for A/B runs)
 ROW_CAP_MIN_BLOCKS = 16
 
 
@@ -199,20 +201,18 @@ class GameBatch:
 
     def _retry_overflow(self, snap, stats, chosen, run, max_retries, orig=None):
         """Lanes whose search overflowed its node / edge pool (stats err bit
-        CIT_ERR_OVERFLOW) are searched again from their pre-search state in a
+        CIT_ERR_OVERFLOW with a CIT_ERR_POOL_* bit) are searched again from their pre-search state in a
         batch of their own, with 4x the tree capacity (the same capacity when
         it was the shared arena that ran out); results and streams are scattered back, and the
         sub-batch is kept so cfr_targets can read those lanes' trees."""
         self._retry = None
-        over = ((stats[:, 4].to(self.device) & ERR_OVERFLOW) != 0).nonzero().flatten()
+        over = ((stats[:, 4].to(self.device) & ERR_POOL) != 0).nonzero().flatten()
         if max_retries <= 0 or over.numel() == 0:
             return chosen, stats
         # 4x caps when a lane reached its own node / edge cap, else the same caps
         # (the retry batch's arena holds every sub-tree's worst case and raw
-        # rows, so a lane that overflowed for another reason cannot again)
-        # (arena out or a diff row past its slot: the same caps, raw rows)
-        st = stats[over.to(stats.device)].cpu().numpy()
-        cap_hit = bool(((st[:, 1] >= self.node_cap - 1) | (st[:, 2] + CFR_EDGE_SLACK >= self.edge_cap)).any())
+        # rows, so a lane stopped by the arena or a diff row cannot be again)
+        cap_hit = bool(((stats[over.to(stats.device), 4] & ERR_POOL_CAP) != 0).any())
         grow = 4 if cap_hit else 1
         g, mt, idx, seer, npm, npi, steps = snap
         sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),

@@ -22,6 +22,7 @@ All device work goes through libcitadels_hip.so (engine.GameBatch); nothing
 here falls back to the CPU.
 """
 import os
+import time
 
 import numpy as np
 import torch
@@ -244,7 +245,8 @@ class _SlicePlanner:
 
 
 def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_cap=None, device=None,
-                   slice_seconds=0.5, max_pool_bytes=None, arena_frac="auto", log=None, overcommit=None):
+                   slice_seconds=0.5, max_pool_bytes=None, arena_frac="auto", log=None, overcommit=None,
+                   max_requeue=0):
     """simulate_games through a tree queue: `slots` trees search at once (one
     per workgroup, sharing one block arena); the search runs in slices of
     ~slice_seconds (cit_cfr_train_slice), and after each slice the finished
@@ -261,13 +263,14 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     of simulate_games bit for bit; trees that overflow are searched again
     through GameBatch.cfr_decide (its retry).  Returns (batch of all seeds,
     stats, targets)."""
-    from .engine import ERR_OVERFLOW, pool_bytes
+    from .engine import ERR_OVERFLOW, ERR_POOL, ERR_POOL_ARENA, ERR_POOL_CAP, pool_bytes
     from . import layout as L
     if node_cap is None:
         node_cap, ec = pool_caps(iters)
         edge_cap = edge_cap or ec
     edge_cap = edge_cap or 5 * node_cap
     dev = torch.device(device or "cuda")
+    t_setup = time.perf_counter()
     src = GameBatch(np.asarray(seeds, np.int64), preset=True, device=dev)
     src.random_position(max_move)
     src.seed_numpy()
@@ -300,6 +303,10 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     sb.arena_frac = arena_f
     sb._pool(node_cap, edge_cap)
     planner = _SlicePlanner(sb, node_cap, edge_cap) if overcommit > 1 else None
+    if log is not None:
+        torch.cuda.synchronize()
+        log("simulate_queue: %d positions and a %d-slot pool set up in %.1f s"
+            % (Q, S, time.perf_counter() - t_setup))
     state = torch.zeros((S, 16), dtype=torch.int32, device=dev)
     chosen = torch.zeros((S, 16), dtype=torch.uint8, device=dev)
     stats = torch.zeros((S, 5), dtype=torch.int32, device=dev)
@@ -310,6 +317,32 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     parts, nxt, n_slices, n_done = [], S, 0, 0
     ticks = max(1, int(slice_seconds * 1e8))
     ran = np.zeros(S, bool)
+    main, side = torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev)
+    rstream = torch.cuda.Stream(device=dev)
+    early = []            # overflowed trees searched again at once, beside the queue: (queue ids, batch, chosen, stats)
+    requeue, retries = [], {}
+    pending = None        # (slots, queue ids) finished last slice: targets extracted during this slice
+    n_requeued = 0
+    # CIT_QUEUE_PROF=1: wall time per phase (synchronising after each; diagnosis only)
+    qprof = {"plan": 0.0, "slice+targets": 0.0, "finish": 0.0} if os.environ.get("CIT_QUEUE_PROF") else None
+
+    def tick(key, t0):
+        if qprof is None:
+            return t0
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        qprof[key] += t1 - t0
+        return t1
+
+    def next_ids(k):
+        nonlocal nxt
+        ids = requeue[:k]
+        del requeue[:k]
+        take = min(k - len(ids), Q - nxt)
+        ids += list(range(nxt, nxt + take))
+        nxt += take
+        return ids
+    tq = time.perf_counter()
     while True:
         running.zero_()
         paused = None
@@ -322,56 +355,136 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
                 paused = torch.from_numpy(np.flatnonzero(pmask)).to(dev)
                 saved = state[paused, 6].clone()
                 state[paused, 6] = CP_DONE           # sits this slice out (the kernel returns at once)
+        tq = tick("plan", tq)
         sb.train_slice(iters, state, ticks, chosen, stats, running)
         n_slices += 1
+        if pending is not None:
+            # last slice's finished trees: their targets are walked on a second stream while this
+            # slice runs (their slots sit this slice out, their blocks stay held until the walk ends)
+            p_slots, p_qs = pending
+            with torch.cuda.stream(side):           # (everything it reads was complete at the last sync)
+                roots = torch.full((S,), -1, dtype=torch.int32, device=dev)
+                roots[p_slots] = _roots_for_targets(out_stats[p_qs])
+                parts.append((sb._cfr_targets(roots, 0), p_slots, p_qs))
+        torch.cuda.synchronize()
+        tq = tick("slice+targets", tq)
         if paused is not None:
             state[paused, 6] = saved
             running += int(paused.numel())         # paused trees are unfinished
+        free = []
+        if pending is not None:
+            p_slots, p_qs = pending
+            src.scatter(sb.subset(p_slots), p_qs)
+            sb.release(p_slots)
+            free.append(p_slots)
+            pending = None
         done = ((state[:, 6] == CP_DONE) & (slot_q >= 0)).nonzero().flatten()
         if done.numel():
             qs = slot_q[done]
-            out_stats[qs] = stats[done]
-            roots = torch.full((S,), -1, dtype=torch.int32, device=dev)
-            roots[done] = _roots_for_targets(stats[done])
-            out_chosen[qs] = chosen[done]
-            parts.append((sb._cfr_targets(roots, 0), done, qs))
-            src.scatter(sb.subset(done), qs)
-            sb.release(done)
-            k = min(int(done.numel()), Q - nxt)
-            if k:
-                new_q = torch.arange(nxt, nxt + k, device=dev)
-                sb.scatter(src.subset(new_q), done[:k])
-                state[done[:k]] = 0
-                if planner is not None:
-                    planner.reset(done[:k].cpu().numpy())
-                slot_q[done[:k]] = new_q
-                nxt += k
-            slot_q[done[k:]] = -1
-            n_done += int(done.numel())
+            st_done = stats[done]
+            # max_requeue > 0: a tree stopped only by the shared arena running out starts again
+            # from its position later in the queue (the same search, bit for bit; at most
+            # max_requeue times, then the final retry)
+            redo = torch.zeros(done.numel(), dtype=torch.bool, device=dev)
+            (n_used, e_used), (n_cap, e_cap) = sb.arena_used() if max_requeue else ((0, 0), (1, 1))
+            if n_used > n_cap or e_used > e_cap:
+                st_np = st_done.cpu().numpy()
+                for i, (q, row) in enumerate(zip(qs.cpu().tolist(), st_np)):
+                    if row[4] == ERR_OVERFLOW | ERR_POOL_ARENA and retries.get(q, 0) < max_requeue:
+                        retries[q] = retries.get(q, 0) + 1
+                        redo[i] = True
+                        requeue.append(q)
+                        n_requeued += 1
+            fin = ~redo
+            ov = fin & ((st_done[:, 4] & ERR_POOL) != 0)        # pool overflows: searched again
+            if bool(ov.any()):
+                early.append(_early_retry(snap, qs[ov], st_done[ov], iters, node_cap, edge_cap, rstream))
+                if log is not None:
+                    log("simulate_queue: tree(s) %s overflowed after slice %d (nodes, edges: %s of caps %d, %d); "
+                        "searched again beside the queue" % (qs[ov].tolist(), n_slices, st_done[ov][:, 1:3].tolist(),
+                                                             node_cap, edge_cap))
+            if bool(fin.any()):
+                out_stats[qs[fin]] = st_done[fin]
+                out_chosen[qs[fin]] = chosen[done[fin]]
+                pending = (done[fin], qs[fin])
+                slot_q[done[fin]] = -2                 # held: targets pending
+                n_done += int(fin.sum())
+            if bool(redo.any()):
+                sb.release(done[redo])
+                free.append(done[redo])
+                slot_q[done[redo]] = -1
             if log is not None:
                 log("simulate_queue: %d of %d trees done after %d slices" % (n_done, Q, n_slices))
-        if int(running.item()) == 0 and bool((slot_q < 0).all()):
+        if free:
+            fs = torch.cat(free)
+            ids = next_ids(int(fs.numel()))
+            k = len(ids)
+            if k:
+                new_q = torch.tensor(ids, dtype=torch.long, device=dev)
+                sb.scatter(src.subset(new_q), fs[:k])
+                state[fs[:k]] = 0
+                if planner is not None:
+                    planner.reset(fs[:k].cpu().numpy())
+                slot_q[fs[:k]] = new_q
+            slot_q[fs[k:]] = -1
+        tq = tick("finish", tq)
+        if int(running.item()) == 0 and pending is None and bool((slot_q < 0).all()) and not requeue:
             break
     if log is not None and planner is not None:
-        log("simulate_queue: %d slots (overcommit %.2f), %d tree-slices paused" % (S, overcommit, planner.paused_slices))
+        log("simulate_queue: %d slots (overcommit %.2f), %d tree-slices paused, %d trees restarted after the "
+            "arena ran out" % (S, overcommit, planner.paused_slices, n_requeued))
+    if log is not None and qprof is not None:
+        log("simulate_queue phases (s): %s over %d slices" % ({k: round(v, 2) for k, v in qprof.items()}, n_slices))
     sb.pool = None
-    over = ((out_stats[:, 4] & ERR_OVERFLOW) != 0).nonzero().flatten()
-    if over.numel():                           # searched again with room to grow (cfr_decide's retry)
-        torch.cuda.empty_cache()
-        g, mt, idx, seer, npm, npi, steps = snap
-        sub = GameBatch.from_tensors(g[over].contiguous(), mt[:, over].contiguous(), idx[over].contiguous(),
-                                     seer[over].contiguous(), npm[:, over].contiguous(), npi[over].contiguous())
-        c2, st2 = sub.cfr_decide(iters, node_cap, edge_cap)
-        out_stats[over] = st2
-        out_chosen[over] = c2
-        extra = sub.cfr_targets(_roots_for_targets(st2), 0)
-        parts.append((extra, torch.arange(sub.B, device=dev), over))
-        src.scatter(sub, over)
-    t = _assemble_targets(parts, Q, exclude=over)
+    t_retry = time.perf_counter()
+    keep_from = len(parts)
+    torch.cuda.synchronize()
+    over = []
+    for oq, sub, c2, st2 in early:
+        # still overflowing (the early search had 4x caps at most): cfr_decide's retries from the snapshot
+        if bool(((st2[:, 4] & ERR_POOL) != 0).any()):
+            g, mt, idx, seer, npm, npi, steps = snap
+            sub = GameBatch.from_tensors(g[oq].contiguous(), mt[:, oq].contiguous(), idx[oq].contiguous(),
+                                         seer[oq].contiguous(), npm[:, oq].contiguous(), npi[oq].contiguous())
+            sub.row_cap = 0
+            c2, st2 = sub.cfr_decide(iters, node_cap, edge_cap)
+        out_stats[oq] = st2
+        out_chosen[oq] = c2
+        parts.append((sub.cfr_targets(_roots_for_targets(st2), 0), torch.arange(sub.B, device=dev), oq))
+        src.scatter(sub, oq)
+        over.append(oq)
+    over = torch.cat(over) if over else torch.zeros(0, dtype=torch.long, device=dev)
+    if log is not None and over.numel():
+        torch.cuda.synchronize()
+        log("simulate_queue: %d trees overflowed and were searched again beside the queue (%.1f s after it)"
+            % (int(over.numel()), time.perf_counter() - t_retry))
+    t = _assemble_targets(parts, Q, exclude=over, keep_from=keep_from)
     t["terminal"] = term
     t["overflow"] = _overflowed(out_stats)
     t["chosen"] = out_chosen
     return src, out_stats, t
+
+
+def _early_retry(snap, oq, st, iters, node_cap, edge_cap, stream):
+    """Trees of queue ids `oq` that overflowed (stats `st`) are searched again
+    at once from their pre-search snapshot, in a batch of their own on
+    `stream` (beside the queue's slices): raw rows, 4x caps when one reached
+    its own caps.  Returns (oq, batch, chosen, stats); results are read after
+    the queue (GameBatch._retry_overflow's rule, without blocking the queue)."""
+    from .engine import ERR_POOL_CAP
+    from . import layout as L
+    g, mt, idx, seer, npm, npi, steps = snap
+    cap_hit = bool(((st[:, 4] & ERR_POOL_CAP) != 0).any())
+    grow = 4 if cap_hit else 1
+    nc = min(grow * node_cap, L.CFR_TBL_MAX * L.CFR_NB)
+    ec = min(grow * edge_cap, L.CFR_TBL_MAX * L.CFR_EB)
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        sub = GameBatch.from_tensors(g[oq].contiguous(), mt[:, oq].contiguous(), idx[oq].contiguous(),
+                                     seer[oq].contiguous(), npm[:, oq].contiguous(), npi[oq].contiguous())
+        sub.row_cap = 0
+        c, s = sub._cfr_decide(iters, nc, ec)
+    return oq, sub, c, s
 
 
 def _overflowed(stats):
@@ -390,10 +503,12 @@ def _roots_for_targets(stats):
     return roots
 
 
-def _assemble_targets(parts, n, exclude=None):
+def _assemble_targets(parts, n, exclude=None, keep_from=None):
     """cfr_targets dicts of trees spread over slot lanes -> one dict in output
     lane order: part (t, slots, ids) holds output lanes `ids` in its lanes
-    `slots`; targets of `exclude` lanes are taken only from the last part."""
+    `slots`; targets of `exclude` lanes are taken only from parts keep_from..
+    (default: the last part)."""
+    keep_from = len(parts) - 1 if keep_from is None else keep_from
     d = parts[0][0]["meta"].device
     metas, firsts, feats, values, dists, opts = [], [], [], [], [], []
     counts = torch.zeros((n, 2), dtype=torch.int32, device=d)
@@ -401,7 +516,7 @@ def _assemble_targets(parts, n, exclude=None):
     for i, (t, slots, ids) in enumerate(parts):
         m = torch.full((t["counts"].shape[0],), -1, dtype=torch.long, device=d)
         m[slots] = ids.long()
-        if exclude is not None and exclude.numel() and i < len(parts) - 1:
+        if exclude is not None and exclude.numel() and i < keep_from:
             m[slots[torch.isin(ids, exclude)]] = -1
         meta = t["meta"].clone()
         lane = m[meta[:, 0].long()]

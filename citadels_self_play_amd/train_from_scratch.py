@@ -5,7 +5,7 @@ process per GPU:
 
 Each data round, every rank runs `--games-per-gpu` simulate_game trees
 (create_a_random_game(100) -> cfr_train(iters, training=True) ->
-get_all_targets) through selfplay.simulate_games (a tree queue over ~640
+get_all_targets) through selfplay.simulate_games (a tree queue over ~1,300
 slots sharing a block arena of ~0.8 of HBM, the least advanced trees paused
 for a slice when it runs short); the (encode_game,
 node_value) pairs are pooled across ranks with an RCCL all-gather until
@@ -24,8 +24,8 @@ ends the run: get_mccfr_targets catches only RanOutOfMemory
 (train_from_scratch.py:56-63).  `--on-error raise` reproduces that (a
 TreeError, a ValueError, on every rank).  The default `drop` keeps going
 without those trees and logs per round how many were dropped and why
-(reference value errors, terminal positions, and pool overflows that
-survived every retry, which have no reference counterpart); none of them
+(reference value errors, terminal positions, and capacity overflows that
+no retry fixes, which have no reference counterpart); none of them
 contributes targets.
 """
 import argparse
@@ -49,8 +49,9 @@ def lane_errors(stats, t, seeds):
     """Per-round error accounting: (value_errors, overflow, terminal, first
     failing seed).  `value_errors` are trees that raised one of the reference's
     exceptions in the search (CIT_ERR_* other than the pool overflow);
-    `overflow` trees outgrew their node pools after every retry (no reference
-    counterpart); `terminal` positions were already over (run_mccfr raises on
+    `overflow` trees hit a fixed capacity the reference does not have (an
+    engine list such as a museum of more than 16 cards, or a node pool after
+    every retry); `terminal` positions were already over (run_mccfr raises on
     them in the reference)."""
     from .engine import ERR_OVERFLOW
     err = stats[:, 4].cpu()
@@ -79,7 +80,7 @@ def collect(rank, world, args, phase, min_targets, log):
                 torch.distributed.all_reduce(bad)          # every rank stops together
             if int(bad.item()):
                 raise TreeError("simulate_game raised in the search (first failing seed on this rank: %s; "
-                                "%d value errors, %d terminal positions, %d pool overflows)"
+                                "%d value errors, %d terminal positions, %d capacity overflows)"
                                 % (first, n_value, n_term, n_over))
         f, v = selfplay.all_gather_targets(t["feat"], t["value"])
         feats.append(f.cpu())
@@ -91,7 +92,7 @@ def collect(rank, world, args, phase, min_targets, log):
         dropped["overflow"] += n_over
         dropped["terminal"] += n_term
         log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), dropped trees on rank %d: %d value "
-            "errors (the reference's ValueError), %d already-terminal positions, %d pool overflows, %.1fs"
+            "errors (the reference's ValueError), %d already-terminal positions, %d capacity overflows, %.1fs"
             % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, rank, n_value, n_term, n_over,
                time.time() - t0))
         rnd += 1

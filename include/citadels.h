@@ -172,6 +172,12 @@ int cit_cfr_arena_reset_rows(void* pool, int B, int node_cap, int edge_cap, int 
 int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
                         hipStream_t stream);
 int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */
+/* Error bits of a search (stats[5*l+4]) beside the engine's CIT_ERR_* bits:
+ * with CIT_ERR_OVERFLOW (0x1), which node-pool capacity ran out -- 0x1000 the
+ * shared arena, 0x2000 the tree's node / edge caps, 0x4000 a diff row slot.
+ * Only these are worth a second search (with more room / raw rows); an
+ * overflow without them is an engine list capacity (e.g. a museum of more
+ * than 16 cards) that no retry fixes. */
 
 /* The config-3 position harness: k = random.randint(lo, hi) drawn from the
  * lane's stream, then k random-policy steps (stops at a winner). */

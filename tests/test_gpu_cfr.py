@@ -112,3 +112,40 @@ def test_gpu_cfr_batch_properties():
     c2, s2 = small.cfr_decide(200)
     assert np.array_equal(c2.cpu().numpy(), out[0][0][::97])
     assert np.array_equal(s2.cpu().numpy()[:, 1:], out[0][1][::97, 1:])
+
+
+def test_gpu_cfr_streams_overlap():
+    """Config-3 batches searched on two HIP streams at once (bench.py's
+    continuous loop) equal the same batches searched one after another:
+    decisions, stats, root games and both streams, bit for bit."""
+    from citadels_self_play_amd.engine import GameBatch
+
+    def make():
+        bs = []
+        for k in range(4):
+            b = GameBatch(np.arange(9_000_000 + 1000 * k, 9_000_000 + 1000 * k + 256), preset=True)
+            b.advance_random(0, 300)
+            b.seed_numpy()
+            b._pool(4096, 5 * 4096)
+            bs.append(b)
+        torch.cuda.synchronize()
+        return bs
+
+    def grab(bs, res):
+        torch.cuda.synchronize()
+        return [(c.cpu().numpy(), s.cpu().numpy(), b.rows(), b.mt.cpu().numpy(), b.np_mt.cpu().numpy())
+                for b, (c, s) in zip(bs, res)]
+
+    alone = make()
+    ref = grab(alone, [b._cfr_decide(200, 4096, 5 * 4096) for b in alone])
+    over = make()
+    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    res = []
+    for k, b in enumerate(over):
+        with torch.cuda.stream(sts[k % 2]):
+            res.append(b._cfr_decide(200, 4096, 5 * 4096))
+    got = grab(over, res)
+    for a, g in zip(ref, got):
+        assert (a[1][:, 4] == 0).mean() > 0.9
+        for x, y in zip(a, g):
+            assert np.array_equal(x, y)

@@ -51,7 +51,10 @@ def test_gpu_config5_200k_queue_golden():
     nc, ec = pool_caps(CFG5_ITERS)
     budget = pool_bytes(32, nc, ec, selfplay.ARENA_FRAC)       # 32 trees at ARENA_FRAC -> 64 slots, overcommit 2
     msgs = []
-    b, stats, t = selfplay.simulate_games(seeds, CFG5_ITERS, max_pool_bytes=budget, log=msgs.append)
+    def log(m):                       # progress on stdout (a long test must not look hung)
+        msgs.append(m)
+        print(m, flush=True)
+    b, stats, t = selfplay.simulate_games(seeds, CFG5_ITERS, max_pool_bytes=budget, log=log)
     assert any("overcommit 2.00" in m for m in msgs), msgs[-3:]    # the queue ran, overcommitted
     stats_np, chosen = stats.cpu().numpy(), t["chosen"].cpu().numpy()
     per = _split(t, len(seeds))

@@ -34,10 +34,10 @@ run_step() {
   case $key in
     tests)
       if [ -n "$val" ]; then
-        (cd "$R" && timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v -k "$val" --timeout 900 \
+        (cd "$R" && timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v -s -k "$val" --timeout 900 \
           --timeout-method thread > "$O/tests.txt" 2>&1)
       else
-        (cd "$R" && timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 900 \
+        (cd "$R" && timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v -s --timeout 900 \
           --timeout-method thread > "$O/tests.txt" 2>&1)
       fi ;;
     smoke)

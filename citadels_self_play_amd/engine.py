@@ -66,6 +66,19 @@ def pool_caps(iters):
 # twice the trees fit in HBM.  A tree with a row past the cap is searched again
 # with raw rows (_retry_overflow).  Small trees (configs 3/4) keep raw rows.
 CFR_ROW_CAP = int(os.environ.get("CIT_ROW_CAP", "128"))      # (0: raw rows everywhere, for A/B runs)
+# cfr_pred splits batches of at least this many trees into 2 stream groups
+PRED_GROUP_MIN = int(os.environ.get("CIT_PRED_GROUP_MIN", "2048"))
+PRED_GROUPS = int(os.environ.get("CIT_PRED_GROUPS", "3"))   # 1 / 2 / 3 / 4: 87.0k / 96.9k / 100.3k / 61.4k decisions/s (config 4, profiles/r03/pred_groups)
+_side_streams = {}
+
+
+def side_streams(device, n):
+    """n HIP streams of `device` kept for reuse (a stream's first launches set up
+    its hardware queue: fresh streams per call would pay that every time)."""
+    key = (str(device), n)
+    if key not in _side_streams:
+        _side_streams[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
+    return _side_streams[key]
 ROW_CAP_MIN_BLOCKS = 16
 
 
@@ -375,6 +388,7 @@ class GameBatch:
         does; a tree that finds it exhausted overflows and is searched again
         (_retry_overflow)."""
         edge_cap = edge_cap or 5 * node_cap
+        self._groups = None                     # a new search: trees live in this batch's pool
         per = self.lib.cit_cfr_pool_bytes(node_cap, edge_cap)
         if per <= 0 or node_cap >= 2 ** 31 or edge_cap >= 2 ** 31:
             raise ValueError("bad node pool capacity (%d nodes, %d edges)" % (node_cap, edge_cap))
@@ -429,16 +443,28 @@ class GameBatch:
         return (int(h[0]), int(h[2])), (int(h[1]), int(h[3]))
 
     def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000, max_retries=3,
-                 flags=0, orig=None):
+                 flags=0, orig=None, groups="auto"):
         """run_mccfr(game, model, max_iterations=iters) with a model and training=False
         (cfr_pred(iters, max_depth) + live action choice) on every lane.  `net` is a
         models.ValueNet; leaf rows of all suspended trees are evaluated in one MFMA
         launch per round.  Trees that outgrow their pool are searched again with
-        a 4x pool (as cfr_decide).  Returns (chosen, stats [B,5], rounds)."""
+        a 4x pool (as cfr_decide).  Returns (chosen, stats [B,5], rounds).
+
+        groups > 1 (auto: PRED_GROUPS = 3 from 2,048 trees): the trees are split into that many
+        sub-batches whose rounds run on their own HIP streams, interleaved, so
+        one group's search kernel fills the SIMDs while another waits for its
+        leaf evaluation and the host's round turnaround (a round lasts as long
+        as its slowest tree); every tree is searched exactly as in one batch."""
         if not hasattr(self, "np_mt"):
             self.seed_numpy()
         snap = self._snapshot() if max_retries > 0 else None
-        chosen, stats, rounds = self._cfr_pred(iters, net, max_depth, node_cap, edge_cap, max_rounds, flags, orig)
+        G = (PRED_GROUPS if self.B >= PRED_GROUP_MIN else 1) if groups == "auto" else max(1, min(int(groups), self.B))
+        if G > 1:
+            chosen, stats, rounds = self._cfr_pred_groups(G, iters, net, max_depth, node_cap, edge_cap, max_rounds,
+                                                          flags, orig)
+        else:
+            self._groups = None
+            chosen, stats, rounds = self._cfr_pred(iters, net, max_depth, node_cap, edge_cap, max_rounds, flags, orig)
         box = [rounds]
 
         def run(sub, nc, ec, mr, o):
@@ -448,35 +474,91 @@ class GameBatch:
         chosen, stats = self._retry_overflow(snap, stats, chosen, run, max_retries, orig)
         return chosen, stats, box[0]
 
-    def _cfr_pred(self, iters, net, max_depth, node_cap, edge_cap, max_rounds, flags=0, orig=None):
+    def _pred_begin(self, node_cap, edge_cap, orig):
+        """Pool and per-tree buffers of a cfr_pred run (state, feat, probs, chosen, waiting)."""
         self._pool(node_cap, edge_cap)
         self._model_tree = True
         d = self.device
-        o = self._orig(orig)
-        state = torch.zeros((self.B, self.lib.cit_cfr_state_bytes() // 4), dtype=torch.int32, device=d)
-        feat = torch.zeros((self.B, 418), dtype=torch.float32, device=d)
-        probs = torch.zeros((self.B, 6), dtype=torch.float32, device=d)
-        chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=d)
-        waiting = torch.zeros(1, dtype=torch.int32, device=d)
-        w = [t.data_ptr() for t in net.w]
+        self._pred = {"o": self._orig(orig),
+                      "state": torch.zeros((self.B, self.lib.cit_cfr_state_bytes() // 4), dtype=torch.int32, device=d),
+                      "feat": torch.zeros((self.B, 418), dtype=torch.float32, device=d),
+                      "probs": torch.zeros((self.B, 6), dtype=torch.float32, device=d),
+                      "chosen": torch.zeros((self.B, 16), dtype=torch.uint8, device=d),
+                      "waiting": torch.zeros(1, dtype=torch.int32, device=d)}
+
+    def _pred_step(self, iters, max_depth, flags):
+        """One cit_cfr_pred_step launch (every tree runs to its next leaf evaluation or its end)."""
+        P = self._pred
+        o = P["o"]
+        P["waiting"].zero_()
+        _lib.check(self.lib.cit_cfr_pred_step(
+            _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
+            _ptr(self.seer), self.B, int(iters), int(flags), None if o is None else _ptr(o), int(max_depth),
+            _ptr(self.pool), self.node_cap, self.edge_cap, _ptr(self.optbuf), _ptr(P["state"]), _ptr(P["probs"]),
+            _ptr(P["feat"]), _ptr(P["chosen"]), _ptr(P["waiting"]), _stream()), "cit_cfr_pred_step")
+
+    def _pred_leaves(self, net):
+        P = self._pred
+        _lib.check(self.lib.cit_mlp_forward(_ptr(P["feat"]), self.B, *[t.data_ptr() for t in net.w], _ptr(P["probs"]),
+                                            None, _stream()), "cit_mlp_forward")
+
+    def _pred_end(self):
+        P = self._pred
+        st = P["state"].cpu()
+        stats = torch.stack([st[:, 8], st[:, 0], st[:, 1], st[:, 3], st[:, 2]], dim=1)
+        return P["chosen"], stats
+
+    def _cfr_pred(self, iters, net, max_depth, node_cap, edge_cap, max_rounds, flags=0, orig=None):
+        self._pred_begin(node_cap, edge_cap, orig)
         rounds = 0
         while rounds < max_rounds:
-            waiting.zero_()
-            _lib.check(self.lib.cit_cfr_pred_step(
-                _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
-                _ptr(self.seer), self.B, int(iters), int(flags), None if o is None else _ptr(o), int(max_depth),
-                _ptr(self.pool), self.node_cap,
-                self.edge_cap,
-                _ptr(self.optbuf), _ptr(state), _ptr(probs), _ptr(feat), _ptr(chosen), _ptr(waiting), _stream()),
-                "cit_cfr_pred_step")
-            if int(waiting.item()) == 0:
+            self._pred_step(iters, max_depth, flags)
+            if int(self._pred["waiting"].item()) == 0:
                 break
-            _lib.check(self.lib.cit_mlp_forward(_ptr(feat), self.B, *w, _ptr(probs), None, _stream()),
-                       "cit_mlp_forward")
+            self._pred_leaves(net)
             rounds += 1
-        st = state.cpu()
-        stats = torch.stack([st[:, 8], st[:, 0], st[:, 1], st[:, 3], st[:, 2]], dim=1)
+        chosen, stats = self._pred_end()
         return chosen, stats, rounds
+
+    def _cfr_pred_groups(self, G, iters, net, max_depth, node_cap, edge_cap, max_rounds, flags, orig):
+        """cfr_pred over G sub-batches on G streams, rounds interleaved (see cfr_pred)."""
+        cur = torch.cuda.current_stream(self.device)
+        parts = [torch.arange(self.B, device=self.device)[g::G] for g in range(G)]
+        o = None if orig is None else np.broadcast_to(np.asarray(orig, np.int32), (self.B,))
+        subs, streams = [], []
+        for g, lanes in enumerate(parts):
+            sub = self.subset(lanes)
+            st = side_streams(self.device, G)[g]
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                sub._pred_begin(node_cap, edge_cap, None if o is None else o[lanes.cpu().numpy()])
+                sub._pred_step(iters, max_depth, flags)
+            subs.append(sub)
+            streams.append(st)
+        rounds = [0] * G
+        active = list(range(G))
+        while active:
+            for g in list(active):
+                sub = subs[g]
+                with torch.cuda.stream(streams[g]):
+                    if int(sub._pred["waiting"].item()) == 0 or rounds[g] >= max_rounds:
+                        active.remove(g)
+                        continue
+                    sub._pred_leaves(net)
+                    rounds[g] += 1
+                    sub._pred_step(iters, max_depth, flags)
+        chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
+        stats = torch.zeros((self.B, 5), dtype=torch.int32)
+        for g, (sub, lanes) in enumerate(zip(subs, parts)):
+            with torch.cuda.stream(streams[g]):
+                c, s = sub._pred_end()
+            cur.wait_stream(streams[g])
+            chosen[lanes] = c
+            stats[lanes.cpu()] = s
+            self.scatter(sub, lanes)
+        self._groups = (parts, subs)
+        self._model_tree = True
+        return chosen, stats, max(rounds)
 
     def lane_batch(self, lane):
         """(batch, lane in it) holding `lane`'s last search tree: the retry
@@ -487,6 +569,13 @@ class GameBatch:
             over = retry[0].cpu().tolist()
             if lane in over:
                 return retry[1].lane_batch(over.index(lane))
+        groups = getattr(self, "_groups", None)
+        if groups is not None:                 # a cfr_pred run split into stream groups
+            parts, subs = groups
+            for lanes, sub in zip(parts, subs):
+                ll = lanes.cpu().tolist()
+                if lane in ll:
+                    return sub.lane_batch(ll.index(lane))
         return self, lane
 
     def tree(self, lane):

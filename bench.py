@@ -352,6 +352,9 @@ def run_rollout(args, world, rank, dev, n_dev, pmc):
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     trans_rank = sum(int(gb.steps.sum().item()) for gb in batches[W:])
     overlapped_ms = float(np.mean(kernel_ms))
+    queue = None
+    if args.queue:
+        queue = _rollout_queue_run(args, world, rank, dev, B, K, trans_rank)
     # One batch resident at a time: the same K batches re-initialised (untimed)
     # and replayed one after another on one stream; the roofline prices these
     # launches (a kernel running alone).
@@ -432,14 +435,18 @@ def run_rollout(args, world, rank, dev, n_dev, pmc):
                     "us_per_step_longest_game": avg_ms * 1e3 / steps_max, "mean_over_max": busy},
         "pmc": pmc})
     n_gpus = min(world, max(1, n_dev))
+    value, ms_step = trans_all / elapsed, elapsed / K * 1e3
+    mode = "streams"
+    if queue is not None:
+        value, ms_step, mode = queue["value"], queue["ms_per_step"], "queue"
     return {
         "metric": "Option.carry_out steps/sec (whole node), 6-player batched self-play",
-        "value": trans_all / elapsed,
+        "value": value,
         "unit": "carry_out transitions/s",
         "n_gpus": n_gpus,
         "steps": K,
         "warmup": W,
-        "ms_per_step": elapsed / K * 1e3,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -456,7 +463,9 @@ def run_rollout(args, world, rank, dev, n_dev, pmc):
         "lane_errors": errs_all,
         "unfinished_lanes": unfinished_all,
         "roofline": roof,
-        "streams": {"n": S, "one_batch": {"value": trans_s_all / el_s, "ms_per_step": el_s / K * 1e3,
+        "mode": mode,
+        "queue": queue,
+        "streams": {"n": S, "value": trans_all / elapsed, "one_batch": {"value": trans_s_all / el_s, "ms_per_step": el_s / K * 1e3,
                                           "same_transitions": trans_s_all == trans_all},
                     "overlapped_launch_avg_ms": overlapped_ms,
                     "note": "K batches launched round-robin on n HIP streams; one_batch replays them one after "
@@ -466,6 +475,38 @@ def run_rollout(args, world, rank, dev, n_dev, pmc):
                 "note": "k_mt_seed_cpython + k_init inside the timed region, init + rollout of batch k on stream "
                         "k %% %d" % S},
     }
+
+
+def _rollout_queue_run(args, world, rank, dev, B, K, trans_ref):
+    """The K timed batches' games (the same seeds) as ONE work queue:
+    cit_rollout_queue with as many one-wave workgroups as the GPU holds; a
+    finished game's slot takes the next game at once.  Returns rank-local
+    timing folded over ranks (max time, summed transitions)."""
+    from citadels_self_play_amd.engine import GameBatch
+    seeds = np.concatenate([np.arange(BASE_SEED + ((args.warmup + k) * world + rank) * B,
+                                      BASE_SEED + ((args.warmup + k) * world + rank) * B + B) for k in range(K)])
+    big = GameBatch(seeds, preset=True, device=dev)
+    warm = GameBatch(np.arange(BASE_SEED - 8192, BASE_SEED), preset=True, device=dev)
+    warm.rollout_queue()
+    torch.cuda.synchronize()
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    _barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record()
+    big.rollout_queue()
+    ev[1].record()
+    torch.cuda.synchronize()
+    _barrier(world)
+    el = time.perf_counter() - t0
+    trans = int(big.steps.sum().item())
+    errs = int((big.errors() != 0).sum().item())
+    el, trans_all, errs = _reduce([el, trans, errs], world, dev, maxes=(0,))
+    return {"value": trans_all / el, "ms_per_step": el / K * 1e3, "kernel_ms": ev[0].elapsed_time(ev[1]),
+            "games": int(len(seeds)) * world, "same_transitions_as_streams": trans == trans_ref,
+            "lane_errors": int(errs),
+            "note": "the K batches' %d games as one work queue (cit_rollout_queue, %d resident waves)"
+                    % (len(seeds), 8 * 4 * torch.cuda.get_device_properties(dev).multi_processor_count)}
 
 
 def _value_net(dev):
@@ -640,6 +681,8 @@ def main():
     ap.add_argument("--games-per-block", type=int, default=0, help="0 = k_rollout_u (one game per workgroup)")
     ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the K timed batches are launched round-robin on (1 = one after another)")
+    ap.add_argument("--queue", action="store_true",
+                    help="config 2: the K timed batches as one work queue (cit_rollout_queue) instead of streams")
     ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per C++ CPU-baseline leg")
     ap.add_argument("--py-seconds", type=float, default=2.0, help="Python-oracle CPU figure")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -28,6 +28,7 @@ _SIGS = {
     "cit_random_choice": ([vp, vp, vp, i32, vp, i32, vp, vp, vp, vp], i32),
     "cit_carry_out": ([vp, vp, vp, i32, vp, vp, vp], i32),
     "cit_rollout_random": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
+    "cit_rollout_queue": ([vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp], i32),
     "cit_encode_games": ([vp, i32, i32, vp, vp], i32),
     "cit_encode_options": ([vp, vp, vp, i32, vp, vp], i32),
     "cit_mlp_forward": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),

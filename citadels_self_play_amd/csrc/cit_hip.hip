@@ -46,10 +46,10 @@ __device__ __forceinline__ CitMT lane_mt(uint32_t* mt, const uint32_t* idx, int 
 #define CIT_LANE0_BODY 0
 #endif
 template <bool MT_LDS, bool STAGE_ROW, class F>
-__device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, F&& body) {
+__device__ __forceinline__ void uniform_game_at(long l, uint32_t* games, uint32_t* mt, uint32_t* idx, int B,
+                                                F&& body) {
   __shared__ __attribute__((aligned(16))) uint32_t row[ROW_W];
   __shared__ uint32_t mts[MT_LDS ? CIT_MT_N : 1];
-  const long l = blockIdx.x;
   if (STAGE_ROW)
     for (int i = threadIdx.x; i < ROW_W; i += blockDim.x) row[i] = games[l * ROW_W + i];
   if (MT_LDS)
@@ -76,6 +76,10 @@ __device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint
   for (int i = threadIdx.x; i < ROW_W; i += blockDim.x) games[l * ROW_W + i] = row[i];
   if (MT_LDS)
     for (int i = threadIdx.x; i < CIT_MT_N; i += blockDim.x) mt[(long)i * B + l] = mts[i];
+}
+template <bool MT_LDS, bool STAGE_ROW, class F>
+__device__ __forceinline__ void uniform_game(uint32_t* games, uint32_t* mt, uint32_t* idx, int B, F&& body) {
+  uniform_game_at<MT_LDS, STAGE_ROW>((long)blockIdx.x, games, mt, idx, B, body);
 }
 
 // init_genrand(19650218), the first step of CPython's init_by_array, is the
@@ -349,6 +353,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROLL_WAVES_P
 #endif
 }
 
+// The same rollout as a work queue (cit_rollout_queue): a grid of as many
+// one-wave workgroups as the GPU holds at once, each taking the next game
+// index from `next` (a vector atomic by lane 0) until all B games are played,
+// so a finished game's slot takes the next game at once instead of idling
+// until the launch's longest game ends.  Every game is played exactly as by
+// k_rollout_u (the same body on the same row and stream).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROLL_WAVES_PER_EU))) void k_rollout_q(
+    uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, int max_steps, int32_t* steps_out,
+    int32_t* winner, int32_t* next) {
+  __shared__ __attribute__((aligned(16))) CitOpt buf[ROLLOUT_BUF ? ROLLOUT_BUF : 1];
+  for (;;) {
+    int g = 0;
+    if (threadIdx.x == 0) g = atomicAdd(next, 1);
+    g = __builtin_amdgcn_readfirstlane(g);
+    if (g >= B) break;                      // every wave reaches this: the grid drains
+    uniform_game_at<true, true>((long)g, games, mt, idx, B, [&](CitGame& gm, CitMT& r, long l) {
+      uint64_t* sc = seer + l * CIT_SEER_MAX;
+      int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
+      int s = 0;
+      while (!gm.terminal && !gm.err && s < cap) {
+        if (ROLLOUT_BUF) cit_random_step_buf(gm, r, sc, buf, ROLLOUT_BUF);
+        else cit_random_step(gm, r, sc);
+        s++;
+      }
+      if (max_steps < 0 && s >= cap && !gm.terminal && !gm.err) gm.err |= CIT_ERR_STEP_CAP;
+      steps_out[l] += s;
+      winner[l] = gm.winner;
+    });
+    __syncthreads();
+  }
+}
+
 // config-3 position harness: k = random.randint(lo, hi) random steps per lane.
 __global__ __launch_bounds__(64) void k_advance(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B,
                                                int lo, int hi, int32_t* steps_out) {
@@ -520,6 +556,16 @@ int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
   }
   // G lanes = G games per workgroup (one wavefront), per-lane code (cit_lanes.hip)
   return cit_rollout_lanes((uint32_t*)games, mt, mt_idx, seer, B, max_steps, games_per_block, steps, winner, stream);
+}
+
+int cit_rollout_queue(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps, int grid,
+                      int32_t* steps, int32_t* winner, int32_t* next, hipStream_t stream) {
+  if (B <= 0 || grid <= 0 || !games || !mt || !mt_idx || !seer || !steps || !winner || !next) return -1;
+  hipError_t e = hipMemsetAsync(next, 0, sizeof(int32_t), stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_rollout_q, dim3(grid < B ? grid : B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, seer,
+                     B, max_steps, steps, winner, next);
+  CHECK_LAUNCH();
 }
 
 int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int lo, int hi,

@@ -190,6 +190,18 @@ class GameBatch:
                                                _stream()), "cit_rollout_random")
         return self.steps, self.winner
 
+    def rollout_queue(self, max_steps=-1, grid=None):
+        """rollout() as a work queue (cit_rollout_queue): `grid` resident waves
+        (default 8 per SIMD of the device) take the games one after another, so
+        a long game no longer holds the launch; same results game by game."""
+        if grid is None:
+            grid = 8 * 4 * torch.cuda.get_device_properties(self.device).multi_processor_count
+        nxt = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_rollout_queue(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.seer),
+                                              self.B, int(max_steps), int(grid), _ptr(self.steps), _ptr(self.winner),
+                                              _ptr(nxt), _stream()), "cit_rollout_queue")
+        return self.steps, self.winner
+
     # --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------------
     def advance_random(self, lo, hi):
         """The config-3 position harness: random.randint(lo, hi) random-policy steps per lane."""

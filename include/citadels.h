@@ -116,6 +116,16 @@ int cit_carry_out(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const CitO
  * 1..64: that many games per wavefront, one per lane. */
 int cit_rollout_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps,
                        int games_per_block, int32_t* steps, int32_t* winner, hipStream_t stream);
+/* The same rollout as a work queue over the B games: `grid` one-wave
+ * workgroups (as many as the GPU holds at once: 8 per SIMD, 8192 on MI355X)
+ * take game indices from the device counter *next (reset to 0 here) until
+ * all are played, so the SIMD slot of a finished game takes the next game at
+ * once (cit_rollout_random's launch lasts as long as its longest game).
+ * Results are those of cit_rollout_random, game by game.  Replaces the same
+ * step loop (compare_to_random.py:37-39, run_utils.py:37-41) over many
+ * games in flight. */
+int cit_rollout_queue(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, int max_steps, int grid,
+                      int32_t* steps, int32_t* winner, int32_t* next, hipStream_t stream);
 
 /* --- featurizers and the value MLP ---------------------------------------- */
 

@@ -243,3 +243,20 @@ def test_gpu_fingerprint_matches_reference(engine, preset):
     off = L.CitGame.points.offset
     pts = b.rows()[:, off:off + 12].copy().view(np.int16).reshape(-1, 6)
     assert int(pts.max(axis=1).sum()) == fp["winner_points"]
+
+
+def test_gpu_rollout_queue_matches_rollout():
+    """cit_rollout_queue (a work queue of one-wave slots) plays every game
+    exactly as cit_rollout_random (one workgroup per game): steps, winners,
+    final rows and streams, bit for bit, on 12,288 games (more than the
+    8,192 slots, so slots take second games)."""
+    from citadels_self_play_amd.engine import GameBatch
+    seeds = np.arange(1_500_000_000, 1_500_000_000 + 12288)
+    a = GameBatch(seeds, preset=True)
+    b = GameBatch(seeds, preset=True)
+    a.rollout()
+    b.rollout_queue()
+    torch.cuda.synchronize()
+    for x, y in ((a.steps, b.steps), (a.winner, b.winner), (a.games, b.games), (a.mt, b.mt), (a.mt_idx, b.mt_idx)):
+        assert torch.equal(x, y)
+    assert int((a.errors() != 0).sum()) == 0 and bool(a.terminal().all())

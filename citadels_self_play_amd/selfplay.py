@@ -101,7 +101,11 @@ def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None):
 ARENA_FRAC = (0.5, 0.8)
 ARENA_MIN_TREES, ARENA_MIN_BLOCKS = 32, 16
 # Tree-queue slots per slot that fits at ARENA_FRAC (simulate_queue's overcommit).
-QUEUE_OVERCOMMIT = 2.0
+# With diff row slots a slot is smaller, so fewer paused trees pay: 1920 trees
+# at cfr_train(200000), two A/B sessions (profiles/r03/overcommit/): 1.0 60.8,
+# 1.25 61.4, 1.5 65.4 / 77.4, 2.0 61.0 (round 2's best), 2.5 63.2, 3.0 60.9
+# trees/s.
+QUEUE_OVERCOMMIT = float(os.environ.get("CIT_QUEUE_OVERCOMMIT", "1.5"))
 
 
 def arena_frac_for(B, node_cap):

@@ -9,7 +9,7 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcitadels_hip.so")
+LIB_PATH = os.environ.get("CIT_LIB_PATH") or os.path.join(HERE, "libcitadels_hip.so")   # override: A/B builds only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "citadels.h")
 
 _lib = None
@@ -32,6 +32,10 @@ _SIGS = {
     "cit_encode_games": ([vp, i32, i32, vp, vp], i32),
     "cit_encode_options": ([vp, vp, vp, i32, vp, vp], i32),
     "cit_mlp_forward": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    "cit_mlp_packed_bytes": ([], u64),
+    "cit_mlp_pack": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    "cit_mlp_work_bytes": ([i32], u64),
+    "cit_mlp_forward_packed": ([vp, i32, vp, vp, vp, vp, u64, vp], i32),
     "cit_cfr_pool_bytes": ([i32, i32], i64),
     "cit_cfr_arena_bytes": ([i32, i32], i64),
     "cit_cfr_block_sizes": ([vp], i32),
@@ -57,6 +61,8 @@ _SIGS = {
     "cit_close_position": ([vp, vp, vp, vp, i32, vp, vp, vp], i32),
     "cit_cfr_pred_step": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp,
                            vp], i32),
+    "cit_cfr_pred_slice": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, i64,
+                            vp, vp, vp], i32),
 }
 
 
@@ -85,7 +91,11 @@ def load():
     import torch  # noqa: F401
     lib = C.CDLL(LIB_PATH)
     for name, (args, res) in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and os.environ.get("CIT_LIB_PATH"):
+            continue                      # an older A/B build without this entry point
+        if fn is None:
+            raise NativeError("%s does not export %s (stale build?)" % (LIB_PATH, name))
         fn.argtypes = args
         fn.restype = res
     _lib = lib

@@ -29,6 +29,14 @@
 #define CFR_OPT_CAP 512
 #ifndef CFR_LBUF
 #define CFR_LBUF 32
+// update_strategy's LDS copies of S / CS (CfrLds.sbuf / cbuf) hold the nodes
+// with up to CFR_SBUF children (at most 55 seen in 64 cfr_train(2000) trees);
+// a node with more runs the host build's loop over its edge records in HBM
+// (the same arithmetic in the same order; CIT_CFR_STRATEGY_HBM forces that
+// path for every node, so a test can compare the two).
+#ifndef CFR_SBUF
+#define CFR_SBUF 96
+#endif
 #endif
 // options listed into LDS per search step
 #define CFR_LN13 0x1.0ca937be1b9dcp-2   // np.log(1.3)
@@ -247,12 +255,15 @@ CIT_HD CitOpt cfr_uopt(const CitOpt& o) { return o; }
 struct CfrLds {
   uint32_t w[2][CIT_GAME_BYTES / 4];
   CitOpt lbuf[CFR_LBUF];
-  double sbuf[CFR_OPT_CAP], cbuf[CFR_OPT_CAP];   // update_strategy: S, CS of node `cnode`
+  double sbuf[CFR_SBUF], cbuf[CFR_SBUF];         // update_strategy: S, CS of node `cnode`
   uint32_t py[CIT_MT_N], np[CIT_MT_N];
   CfrTree T;
   CfrState S;
   int cnode, cnch;                                // node (and its child count) whose normalised CS is in cbuf (-1: none)
-  uint8_t tmp[CIT_SAMPLE_SCRATCH];
+  int sbuf_on;                                    // 0 under CIT_CFR_STRATEGY_HBM
+  // cit_sample_private's scratch is read and written 16 bytes at a time:
+  // keep it 16-byte aligned whatever the fields above add up to
+  __attribute__((aligned(16))) uint8_t tmp[CIT_SAMPLE_SCRATCH];
 };
 static __shared__ __attribute__((aligned(16))) CfrLds cfr_ls;
 // Dynamic LDS of a search launch (sized per launch, cfr_dyn_lds_bytes): the
@@ -978,12 +989,11 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
   if (nch == 0) return;
   CfrEdge* E = cfr_edge(T, N.first_edge);
 #if CIT_WAVE
-  if (!(N.flags & NF_ROLE_PICK)) {
+  if (!(N.flags & NF_ROLE_PICK) && nch <= CFR_SBUF && cfr_ls.sbuf_on) {
     // lane a (a + 64, ...) owns edge a; the numpy sums run in their serial
     // order over LDS copies (cbuf keeps the normalised CS for cfr_choose)
     double* sb = cfr_ls.sbuf;
     double* cb = cfr_ls.cbuf;
-    if (nch > CFR_OPT_CAP) { T.err |= CIT_ERR_OVERFLOW; return; }
     const int l = CFR_LANE;
     for (int a = l; a < nch; a += 64) sb[a] = exp((-E[a].R) * CFR_LN13);
     CFR_SYNC();
@@ -1006,6 +1016,7 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
     cfr_ls.cnch = nch;
     return;
   }
+  cfr_ls.cnode = -1;
 #endif
   if (!(N.flags & NF_ROLE_PICK)) {
     for (int a = 0; a < nch; a++) E[a].S = exp((-E[a].R) * CFR_LN13);
@@ -1300,10 +1311,12 @@ CIT_NOINLINE void cfr_write_feat(CfrTree& T_in, int n, float* feat) {
 }
 
 // One resumption.  Working row 0 must hold the lane's game when S.phase ==
-// CP_INIT.  Returns 1 when suspended for an evaluation, 0 when done (S.phase
+// CP_INIT.  Returns 1 when suspended for an evaluation, 2 when `bud` ran out
+// at an iteration boundary (S.phase stays CP_RUN: the next resumption goes
+// on from S.cur / S.it exactly where this one stopped), 0 when done (S.phase
 // == CP_DONE).
 CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_depth, const float* probs_in,
-                              float* feat, CitOpt& chosen, bool root_skipped = false) {
+                              float* feat, CitOpt& chosen, bool root_skipped = false, CfrBudget* bud = nullptr) {
   CfrTree& T = CFR_T(T_in);
   CfrState& S = CFR_S(S_in);
   iters = cfr_u(iters);
@@ -1335,7 +1348,9 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
     S.it++;
     S.phase = CP_RUN;
   }
+  const int first = cfr_u(S.it);
   while (S.it < iters && !T.err) {
+    if (bud && S.it > first && cfr_budget_spent(*bud)) return 2;
     cfr_update_strategy(T, S.cur);
     int a = cfr_u(cfr_choose(T, S.cur));
     if (T.err) break;

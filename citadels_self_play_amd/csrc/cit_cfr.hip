@@ -41,9 +41,10 @@ __device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, 
 // streams, working rows.
 __device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx,
                                            uint64_t* seer, int B, long l, uint8_t* pool, int node_cap, int edge_cap,
-                                           CitOpt* optbuf) {
+                                           CitOpt* optbuf, int flags) {
   CfrTree& T = cfr_ls.T;
   cfr_ls.cnode = -1;
+  cfr_ls.sbuf_on = (flags & CIT_CFR_STRATEGY_HBM) ? 0 : 1;
   cfr_tree_bind(T, pool, B, l, node_cap, edge_cap);
   T.nbt = nullptr;          // the tables live in dynamic LDS (cfr_nbt_at / cfr_ebt_at)
   T.ebt = nullptr;
@@ -76,9 +77,23 @@ __device__ __forceinline__ void tables_store(const CfrTree& T) {
   for (int i = threadIdx.x; i < T.n_eblk; i += blockDim.x) T.ebt_hbm[i] = cfr_ebt_at(T, i);
 }
 
+// CFR_WAVES_PER_EU (compile-time) bounds the search kernels' VGPRs so that
+// many trees share a SIMD (the search is latency-bound, one tree per wave);
+// 0 leaves the register budget to the compiler.  3 (<= 168 VGPRs, no
+// spills) with the 13 KB LDS block = 12 trees per CU instead of 7: config 4
+// 98.4 k -> 102.2 k decisions/s, config 3 unchanged (profiles/r03/occupancy/).
+#ifndef CFR_WAVES_PER_EU
+#define CFR_WAVES_PER_EU 3
+#endif
+#if CFR_WAVES_PER_EU
+#define CFR_OCC __attribute__((amdgpu_waves_per_eu(CFR_WAVES_PER_EU)))
+#else
+#define CFR_OCC
+#endif
+
 // One MCCFR decision per workgroup: a 64-lane team runs the search on its
 // tree (node pool in HBM, working state in LDS).
-__global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
+__global__ __launch_bounds__(64) CFR_OCC void k_cfr_decide(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
                                                    uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
                                                    const int32_t* orig, uint8_t* pool,
                                                    int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen,
@@ -90,7 +105,7 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
 #endif
   cfr_prof_reset();
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf);
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags);
   T.n_nodes = T.n_edges = 0;
   T.err = 0;
   T.carry_outs = 0;
@@ -123,19 +138,25 @@ __global__ __launch_bounds__(64) void k_cfr_decide(uint32_t* games, uint32_t* mt
 }
 
 // One resumption of cfr_pred (cit_cfr.h: cfr_pred_run) per tree; lane 0 adds
-// 1 to *waiting when the tree suspends for a leaf evaluation.
-__global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
+// 1 to *waiting when the tree suspends for a leaf evaluation, 1 to *running
+// when `ticks` of the wall clock (0 = no limit) ran out first.
+__global__ __launch_bounds__(64) CFR_OCC void k_cfr_pred_step(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
                                                       uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
                                                       const int32_t* orig, int max_depth, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
                                                       CfrState* state, const float* probs, float* feat,
-                                                      CitOpt* chosen, int32_t* waiting) {
+                                                      CitOpt* chosen, int32_t* waiting, uint64_t ticks,
+                                                      int32_t* running) {
   long l = blockIdx.x;
   if (l >= B) return;
+  CfrBudget bud;
+  bud.t0 = wall_clock64();
+  bud.ticks = ticks;
+  bud.iters_left = 0;
   CfrState& S = cfr_ls.S;
   S = state[l];             // every lane stores the same value
   if (S.phase == CP_DONE) return;
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf);
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags);
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;
@@ -148,7 +169,7 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
   }
   CitOpt c;
   int r = cfr_pred_run(T, S, iters, max_depth, probs + 6 * l, feat + (long)CIT_FEAT * l, c,
-                       (flags & CIT_CFR_ROOT_SKIPPED) != 0);
+                       (flags & CIT_CFR_ROOT_SKIPPED) != 0, ticks ? &bud : nullptr);
   r = cfr_u(r);
   cfr_state_save(T, S);
   if (!r && S.root >= 0) row_load(T, games + l * ROW_W, S.root);
@@ -160,7 +181,8 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
     if (!r) chosen[l] = c;
     idx[l] = T.py.pos;
     npidx[l] = T.np.pos;
-    if (r) atomicAdd(waiting, 1);
+    if (r == 1) atomicAdd(waiting, 1);
+    if (r == 2) atomicAdd(running, 1);
   }
 }
 
@@ -168,7 +190,7 @@ __global__ __launch_bounds__(64) void k_cfr_pred_step(uint32_t* games, uint32_t*
 // tree resumes from its CfrState and runs until `ticks` of the wall clock
 // have passed (then lane 0 adds 1 to *running) or it is done (then as
 // k_cfr_decide: live choice, root game back into games[l], chosen, stats).
-__global__ __launch_bounds__(64) void k_cfr_train_slice(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
+__global__ __launch_bounds__(64) CFR_OCC void k_cfr_train_slice(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
                                                         uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
                                                         const int32_t* orig, uint8_t* pool, int node_cap, int edge_cap,
                                                         CitOpt* optbuf, CfrState* state, uint64_t ticks,
@@ -183,7 +205,7 @@ __global__ __launch_bounds__(64) void k_cfr_train_slice(uint32_t* games, uint32_
   S = state[l];
   if (S.phase == CP_DONE) return;
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf);
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags);
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;
@@ -359,7 +381,23 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
     return -1;
   hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
                      seer, B, iters, flags, orig_player, max_depth, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
-                     (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting);
+                     (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting, (uint64_t)0, (int32_t*)nullptr);
+  CHECK_LAUNCH();
+}
+
+int cit_cfr_pred_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                       int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,
+                       int node_cap, int edge_cap, CitOption* optbuf, void* state, const float* probs, float* feat,
+                       CitOption* chosen, int64_t slice_ticks, int32_t* waiting, int32_t* running,
+                       hipStream_t stream) {
+  if (B <= 0 || iters < 0 || slice_ticks < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt ||
+      !mt_idx || !np_mt || !np_idx || !seer || !pool || !optbuf || !state || !probs || !feat || !chosen ||
+      !waiting || (slice_ticks && !running))
+    return -1;
+  hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream,
+                     (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer, B, iters, flags, orig_player, max_depth,
+                     (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CfrState*)state, probs, feat,
+                     (CitOpt*)chosen, waiting, (uint64_t)slice_ticks, running);
   CHECK_LAUNCH();
 }
 

@@ -4,11 +4,19 @@
 //   wp = square_and_normalize(fc4(relu(fc3(relu(fc2'(relu(fc1'(x))))))))
 //        (models.py:17-24, train_utils.py:143-145, deep_mccfr.py:364-374)
 //
-// One workgroup = 16 waves = a 16-row batch tile; every layer is a chain of
-// v_mfma_f32_16x16x4_f32 (exact f32: a k-ordered fmaf chain per output,
-// starting from 0, then + bias, then ReLU), activations staged in LDS,
-// weights pre-transposed to [k][n] so a quarter-wave reads 64 contiguous bytes.
-// fc4 (6 outputs) runs as one padded 16-column tile.
+// Every layer is a chain of v_mfma_f32_16x16x4_f32 per 16x16 output tile
+// (exact f32: a k-ordered fmaf chain per output, starting from 0, then + bias,
+// then ReLU), inputs staged in LDS, weights pre-transposed to [k][n] so a
+// quarter-wave reads 64 contiguous bytes.  fc4 (6 outputs) runs as one padded
+// 16-column tile.  Two schedules of the same chains (bitwise equal outputs):
+//  * k_mlp: one workgroup = 16 waves = a 16-row batch tile through all four
+//    layers (no workspace; one CU per 16 rows, so a call under 4,096 rows
+//    leaves CUs idle and costs one CU's four-layer latency, ~42 us);
+//  * k_mlp_layer x2 + k_mlp_head (cit_mlp_forward_packed): fc1 and fc2
+//    spread their 16x16 tiles over 4-wave workgroups (one tile per wave,
+//    rows x column groups), H1 / H2 through a caller workspace, then fc3 +
+//    fc4 + square_and_normalize per 16-row tile; weights MFMA-packed once by
+//    cit_mlp_pack (one 16-byte load per lane per four MFMAs).
 // One row per lane (the featurizer kernels): no wave-uniform engine scans.
 #define CIT_NO_WAVE 1
 #include <hip/hip_runtime.h>
@@ -40,44 +48,56 @@ namespace {
 // register ring) so the per-lane 4-byte L2 loads overlap the MFMAs.
 #define MLP_PF 6
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-template <int K, int N, int NT>
+template <int K, int N, int NT, int PF = MLP_PF>
 __device__ __forceinline__ void tile16_layer(const float* in, int in_s, const float* __restrict__ WT,
                                              const float* __restrict__ bias, float* out, int out_s, int n0,
-                                             bool relu, int nvalid) {
+                                             bool relu, int nvalid, int nrows = 16) {
   constexpr int KK = (K + 3) / 4;
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   f32x4 acc[NT];
-  int col[NT];
+  int col[NT], colc[NT];
   bool cv[NT];
 #pragma unroll
   for (int t = 0; t < NT; t++) {
     for (int i = 0; i < 4; i++) acc[t][i] = 0.0f;
     col[t] = n0 + 16 * t + r;
     cv[t] = col[t] < nvalid;
+    colc[t] = cv[t] ? col[t] : nvalid - 1;
   }
+  // both operands run PF steps ahead in register rings (the LDS activation
+  // read as well as the L2 weight read), so an MFMA never waits on a load
+  // issued in its own step.  Operands past K (or past the valid columns)
+  // read a clamped in-bounds address and are zeroed when consumed, not when
+  // loaded (a select at load time would wait for the load).
   auto wgt = [&](int t, int kk) -> float {
-    int k = 4 * kk + q;
-    return (k < K && cv[t]) ? WT[(long)k * N + col[t]] : 0.0f;
+    const int k = 4 * kk + q;
+    return WT[(long)(k < K ? k : K - 1) * N + colc[t]];
   };
   const float* ip = in + r * in_s + q;
-  float b[MLP_PF][NT];
+  auto act = [&](int kk) -> float { return ip[4 * (4 * kk + q < K ? kk : 0)]; };
+  float b[PF][NT], av[PF];
 #pragma unroll
-  for (int i = 0; i < MLP_PF; i++)
+  for (int i = 0; i < PF; i++) {
+    av[i] = act(i);
 #pragma unroll
-    for (int t = 0; t < NT; t++) b[i][t] = i < KK ? wgt(t, i) : 0.0f;
-  for (int k0 = 0; k0 < KK; k0 += MLP_PF) {
+    for (int t = 0; t < NT; t++) b[i][t] = wgt(t, i);
+  }
+  for (int k0 = 0; k0 < KK; k0 += PF) {
 #pragma unroll
-    for (int i = 0; i < MLP_PF; i++) {
+    for (int i = 0; i < PF; i++) {
       const int kk = k0 + i;
       if (kk < KK) {
-        float a = 4 * kk + q < K ? ip[4 * kk] : 0.0f;
+        const bool kv = 4 * kk + q < K;
+        const float a = kv ? av[i] : 0.0f;
+        av[i] = act(kk + PF);
 #pragma unroll
         for (int t = 0; t < NT; t++) {
-          float bn = kk + MLP_PF < KK ? wgt(t, kk + MLP_PF) : 0.0f;
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[i][t], acc[t], 0, 0, 0);
-          b[i][t] = bn;
+          const float w = kv && cv[t] ? b[i][t] : 0.0f;
+          b[i][t] = wgt(t, kk + PF);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w, acc[t], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);   // keep each step's prefetches in that step
       }
     }
   }
@@ -87,9 +107,35 @@ __device__ __forceinline__ void tile16_layer(const float* in, int in_s, const fl
     float bb = bias[col[t]];
     for (int i = 0; i < 4; i++) {
       int row = 4 * q + i;
+      if (row >= nrows) continue;
       float v = acc[t][i] + bb;
       out[row * out_s + col[t]] = relu ? (v > 0.0f ? v : 0.0f) : v;
     }
+  }
+}
+
+// Rows m0.. of a [M][K] matrix into LDS: element (r, k < KP) of the tile
+// goes to X[dst(r, k)] (zero past K or past the valid rows).  Every thread's
+// loads are issued before any is waited on (clamped in-bounds addresses,
+// then a select): a load-wait-store loop would pay one L2/HBM latency per
+// element.
+template <int K, int KP, int NTH, class Dst>
+__device__ __forceinline__ void mlp_stage(const float* __restrict__ in, int m0, int nrows, float* X, Dst dst) {
+  constexpr int TOT = MLP_ROWS * KP, IT = (TOT + NTH - 1) / NTH;
+  float v[IT];
+#pragma unroll
+  for (int it = 0; it < IT; it++) {
+    const int i = threadIdx.x + it * NTH;
+    const int r = i / KP, k = i - r * KP;
+    const int rc = r < nrows ? r : nrows - 1, kc = k < K ? k : K - 1;
+    const float x = in[(long)(m0 + rc) * K + kc];
+    v[it] = (i < TOT && r < nrows && k < K) ? x : 0.0f;
+  }
+#pragma unroll
+  for (int it = 0; it < IT; it++) {
+    const int i = threadIdx.x + it * NTH;
+    const int r = i / KP, k = i - r * KP;
+    if (i < TOT) X[dst(r, k)] = v[it];
   }
 }
 
@@ -111,10 +157,7 @@ __global__ __launch_bounds__(64 * MLP_WAVES) void k_mlp(const float* __restrict_
   const int m0 = blockIdx.x * MLP_ROWS;
   const int nrows = min(MLP_ROWS, M - m0);
   const int wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < MLP_ROWS * MLP_IN; i += blockDim.x) {
-    int r = i / MLP_IN, k = i - r * MLP_IN;
-    X[r * MLP_XS + k] = r < nrows ? feat[(long)(m0 + r) * MLP_IN + k] : 0.0f;
-  }
+  mlp_stage<MLP_IN, MLP_IN, 64 * MLP_WAVES>(feat, m0, nrows, X, [](int r, int k) { return r * MLP_XS + k; });
   __syncthreads();
   tile16_layer<MLP_IN, MLP_H1, 2>(X, MLP_XS, w1t, b1, H1, MLP_H1S, wave * 32, true, MLP_H1);
   __syncthreads();
@@ -135,6 +178,175 @@ __global__ __launch_bounds__(64 * MLP_WAVES) void k_mlp(const float* __restrict_
       if (logits) logits[(long)(m0 + r) * MLP_OUT + j] = v;
     }
     for (int j = 0; j < MLP_OUT; j++) probs[(long)(m0 + r) * MLP_OUT + j] = sq[j] / s;
+  }
+}
+
+// ---------------------------------------------------------------- packed path
+// The layer-split schedule reads MFMA-packed weights (cit_mlp_pack): for a
+// layer (K, N), 16-column tile nt and k-group g (4 MFMA steps = 16 k), lane
+// l = 16 q + r holds the float4 {W[16 g + 4 j + q][16 nt + r], j = 0..3}
+// (zero past K or N), so one 16-byte load per lane feeds four chained MFMAs
+// and a wave's load is 1 KB contiguous.  The 16 input rows sit in LDS in the
+// matching order (row r: group g, quarter q, step j at (4 g + q) * 4 + j), so
+// the activation operand is one ds_read_b128 per group as well.  The k order
+// of every chain is unchanged (k ascending, zero padding only past K): the
+// outputs are bitwise those of k_mlp / the fmaf oracle.
+__host__ __device__ constexpr int mlp_kg(int K) { return ((K + 3) / 4 + 3) / 4; }
+__host__ __device__ constexpr int mlp_ps(int K) { return mlp_kg(K) * 16 + 4; }   // LDS row stride (floats)
+#define MLP_P1 0
+#define MLP_P2 (MLP_P1 + (MLP_H1 / 16) * mlp_kg(MLP_IN) * 256)
+#define MLP_P3 (MLP_P2 + (MLP_H2 / 16) * mlp_kg(MLP_H1) * 256)
+#define MLP_P4 (MLP_P3 + (MLP_H3 / 16) * mlp_kg(MLP_H2) * 256)
+#define MLP_PB1 (MLP_P4 + mlp_kg(MLP_H3) * 256)
+#define MLP_PB2 (MLP_PB1 + MLP_H1)
+#define MLP_PB3 (MLP_PB2 + MLP_H2)
+#define MLP_PB4 (MLP_PB3 + MLP_H3)
+#define MLP_PTOTAL (MLP_PB4 + 16)
+
+__device__ __forceinline__ float mlp_pack_w(const float* W, int K, int N, long e) {
+  const int j = (int)(e & 3), l = (int)((e >> 2) & 63);
+  const long rest = e >> 8;
+  const int kg = mlp_kg(K);
+  const int g = (int)(rest % kg), nt = (int)(rest / kg);
+  const int k = 16 * g + 4 * j + (l >> 4), c = 16 * nt + (l & 15);
+  return (k < K && c < N) ? W[(long)k * N + c] : 0.0f;
+}
+
+__global__ void k_mlp_pack(const float* __restrict__ w1t, const float* __restrict__ b1, const float* __restrict__ w2t,
+                           const float* __restrict__ b2, const float* __restrict__ w3t, const float* __restrict__ b3,
+                           const float* __restrict__ w4t, const float* __restrict__ b4, float* __restrict__ P) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= MLP_PTOTAL) return;
+  float v;
+  if (i < MLP_P2) v = mlp_pack_w(w1t, MLP_IN, MLP_H1, i - MLP_P1);
+  else if (i < MLP_P3) v = mlp_pack_w(w2t, MLP_H1, MLP_H2, i - MLP_P2);
+  else if (i < MLP_P4) v = mlp_pack_w(w3t, MLP_H2, MLP_H3, i - MLP_P3);
+  else if (i < MLP_PB1) v = mlp_pack_w(w4t, MLP_H3, MLP_OUT, i - MLP_P4);
+  else if (i < MLP_PB2) v = b1[i - MLP_PB1];
+  else if (i < MLP_PB3) v = b2[i - MLP_PB2];
+  else if (i < MLP_PB4) v = b3[i - MLP_PB3];
+  else v = i - MLP_PB4 < MLP_OUT ? b4[i - MLP_PB4] : 0.0f;
+  P[i] = v;
+}
+
+// Rows m0.. into LDS in the packed activation order (row r: group g,
+// quarter q, step j at (4 g + q) * 4 + j).
+template <int K, int NTH>
+__device__ __forceinline__ void mlp_stage_packed(const float* __restrict__ in, int m0, int nrows, float* X) {
+  constexpr int S = mlp_ps(K);
+  mlp_stage<K, mlp_kg(K) * 16, NTH>(in, m0, nrows, X, [](int r, int k) {
+    return r * S + ((k >> 4) * 4 + (k & 3)) * 4 + ((k >> 2) & 3);
+  });
+}
+
+// One 16x16 output tile (column tile nt of a (K, N) layer) as a chain of
+// 4 * mlp_kg(K) MFMAs; both operands run PFG groups ahead in register rings.
+template <int K, int PFG>
+__device__ __forceinline__ f32x4 mlp_tile_packed(const float* X, const float* __restrict__ Wl, int nt) {
+  constexpr int KG = mlp_kg(K), S = mlp_ps(K);
+  const int lane = threadIdx.x & 63;
+  const f32x4* xa = reinterpret_cast<const f32x4*>(X + (lane & 15) * S + (lane >> 4) * 4);   // + 4 g (float4 units)
+  const f32x4* wb = reinterpret_cast<const f32x4*>(Wl) + (long)nt * KG * 64 + lane;          // + 64 g
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  f32x4 a[PFG], w[PFG];
+#pragma unroll
+  for (int i = 0; i < PFG; i++) {
+    const int g = i < KG ? i : KG - 1;
+    a[i] = xa[4 * g];
+    w[i] = wb[64 * g];
+  }
+  for (int g0 = 0; g0 < KG; g0 += PFG) {
+#pragma unroll
+    for (int i = 0; i < PFG; i++) {
+      const int g = g0 + i;
+      if (g < KG) {
+        const f32x4 ac = a[i], wc = w[i];
+        const int gn = g + PFG < KG ? g + PFG : KG - 1;
+        a[i] = xa[4 * gn];
+        w[i] = wb[64 * gn];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ac.x, wc.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ac.y, wc.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ac.z, wc.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ac.w, wc.w, acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);   // keep each group's prefetches in that group
+      }
+    }
+  }
+  return acc;
+}
+
+// fc1 / fc2 as their own launches: blockIdx.x = 16-row tile, blockIdx.y = a
+// group of four 16-column tiles, one per wave (a 1,024-row call is 512
+// workgroups for fc1, 256 for fc2); output rows [M][N] (+ bias, ReLU).
+#define MLP_LAYER_WAVES 4
+#define MLP_PFG 8
+template <int K, int N>
+__global__ __launch_bounds__(64 * MLP_LAYER_WAVES) void k_mlp_layer(const float* __restrict__ in, int M,
+                                                                   const float* __restrict__ Wl,
+                                                                   const float* __restrict__ bias,
+                                                                   float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float X[MLP_ROWS * mlp_ps(K)];
+  const int m0 = blockIdx.x * MLP_ROWS;
+  const int nrows = min(MLP_ROWS, M - m0);
+  mlp_stage_packed<K, 64 * MLP_LAYER_WAVES>(in, m0, nrows, X);
+  __syncthreads();
+  const int nt = blockIdx.y * MLP_LAYER_WAVES + (threadIdx.x >> 6);
+  if (nt * 16 >= N) return;
+  const f32x4 acc = mlp_tile_packed<K, MLP_PFG>(X, Wl, nt);
+  const int lane = threadIdx.x & 63, col = nt * 16 + (lane & 15), q = lane >> 4;
+  const float bb = bias[col];
+  for (int i = 0; i < 4; i++) {
+    const int row = 4 * q + i;
+    if (row < nrows) {
+      const float v = acc[i] + bb;
+      out[(long)(m0 + row) * N + col] = v > 0.0f ? v : 0.0f;
+    }
+  }
+}
+
+// fc3 (8 column tiles, one per wave; H3 written to LDS in the packed order)
+// + fc4 (wave 0) + square_and_normalize for one 16-row tile of H2.
+#define MLP_HEAD_WAVES (MLP_H3 / 16)
+__global__ __launch_bounds__(64 * MLP_HEAD_WAVES) void k_mlp_head(const float* __restrict__ h2, int M,
+                                                                 const float* __restrict__ P,
+                                                                 float* __restrict__ probs,
+                                                                 float* __restrict__ logits) {
+  __shared__ __attribute__((aligned(16))) float X2[MLP_ROWS * mlp_ps(MLP_H2)];
+  __shared__ __attribute__((aligned(16))) float X3[MLP_ROWS * mlp_ps(MLP_H3)];
+  __shared__ float L[MLP_ROWS * 8];
+  const int m0 = blockIdx.x * MLP_ROWS;
+  const int nrows = min(MLP_ROWS, M - m0);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  mlp_stage_packed<MLP_H2, 64 * MLP_HEAD_WAVES>(h2, m0, nrows, X2);
+  __syncthreads();
+  {
+    const f32x4 acc = mlp_tile_packed<MLP_H2, MLP_PFG>(X2, P + MLP_P3, wave);
+    const int c = wave * 16 + r;
+    const float bb = P[MLP_PB3 + c];
+    for (int i = 0; i < 4; i++) {
+      const float v = acc[i] + bb;
+      X3[(4 * q + i) * mlp_ps(MLP_H3) + ((c >> 4) * 4 + (c & 3)) * 4 + ((c >> 2) & 3)] = v > 0.0f ? v : 0.0f;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const f32x4 acc = mlp_tile_packed<MLP_H3, MLP_PFG>(X3, P + MLP_P4, 0);
+    if (r < MLP_OUT) {
+      const float bb = P[MLP_PB4 + r];
+      for (int i = 0; i < 4; i++) L[(4 * q + i) * 8 + r] = acc[i] + bb;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nrows) {
+    const int rr = threadIdx.x;
+    float sq[MLP_OUT], s = 0.0f;
+    for (int j = 0; j < MLP_OUT; j++) {
+      const float v = L[rr * 8 + j];
+      sq[j] = v * v;
+      s += sq[j];
+      if (logits) logits[(long)(m0 + rr) * MLP_OUT + j] = v;
+    }
+    for (int j = 0; j < MLP_OUT; j++) probs[(long)(m0 + rr) * MLP_OUT + j] = sq[j] / s;
   }
 }
 
@@ -193,6 +405,35 @@ int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1,
   }
   hipLaunchKernelGGL(k_mlp, dim3((M + MLP_ROWS - 1) / MLP_ROWS), dim3(64 * MLP_WAVES), mlp_lds(), stream, feat, M, w1t, b1, w2t,
                      b2, w3t, b3, w4t, b4, probs, logits);
+  CHECK_LAUNCH();
+}
+
+size_t cit_mlp_packed_bytes(void) { return (size_t)MLP_PTOTAL * sizeof(float); }
+
+int cit_mlp_pack(const float* w1t, const float* b1, const float* w2t, const float* b2, const float* w3t,
+                 const float* b3, const float* w4t, const float* b4, void* packed, hipStream_t stream) {
+  if (!w1t || !b1 || !w2t || !b2 || !w3t || !b3 || !w4t || !b4 || !packed) return -1;
+  hipLaunchKernelGGL(k_mlp_pack, dim3((MLP_PTOTAL + 255) / 256), dim3(256), 0, stream, w1t, b1, w2t, b2, w3t, b3, w4t,
+                     b4, (float*)packed);
+  CHECK_LAUNCH();
+}
+
+size_t cit_mlp_work_bytes(int M) { return M > 0 ? (size_t)M * (MLP_H1 + MLP_H2) * sizeof(float) : 0; }
+
+int cit_mlp_forward_packed(const float* feat, int M, const void* packed, float* probs, float* logits, void* work,
+                           size_t work_bytes, hipStream_t stream) {
+  if (M < 0 || (M && (!feat || !packed || !probs))) return -1;
+  if (!M) return 0;
+  if (!work || work_bytes < cit_mlp_work_bytes(M)) return -1;
+  const float* P = (const float*)packed;
+  float* h1 = (float*)work;
+  float* h2 = h1 + (size_t)M * MLP_H1;
+  const int tiles = (M + MLP_ROWS - 1) / MLP_ROWS;
+  hipLaunchKernelGGL((k_mlp_layer<MLP_IN, MLP_H1>), dim3(tiles, MLP_H1 / (16 * MLP_LAYER_WAVES)),
+                     dim3(64 * MLP_LAYER_WAVES), 0, stream, feat, M, P + MLP_P1, P + MLP_PB1, h1);
+  hipLaunchKernelGGL((k_mlp_layer<MLP_H1, MLP_H2>), dim3(tiles, MLP_H2 / (16 * MLP_LAYER_WAVES)),
+                     dim3(64 * MLP_LAYER_WAVES), 0, stream, h1, M, P + MLP_P2, P + MLP_PB2, h2);
+  hipLaunchKernelGGL(k_mlp_head, dim3(tiles), dim3(64 * MLP_HEAD_WAVES), 0, stream, h2, M, P, probs, logits);
   CHECK_LAUNCH();
 }
 

@@ -34,6 +34,7 @@ ERR_POOL = ERR_POOL_ARENA | ERR_POOL_CAP | ERR_POOL_ROW
 EDGE_DT = np.dtype([("opt", "u1", 16), ("child", "<i4"), ("pad", "<i4"), ("R", "<f8"), ("S", "<f8"), ("CS", "<f8")])
 WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])   # role-pick columns (csrc/cit_cfr.h)
 CFR_ROOT_SKIPPED = 1       # CIT_CFR_ROOT_SKIPPED (include/citadels.h)
+CFR_STRATEGY_HBM = 2       # CIT_CFR_STRATEGY_HBM: update_strategy without the LDS copies (checking aid)
 
 
 def node_arrays(nodes, edges, n):
@@ -68,7 +69,10 @@ def pool_caps(iters):
 CFR_ROW_CAP = int(os.environ.get("CIT_ROW_CAP", "128"))      # (0: raw rows everywhere, for A/B runs)
 # cfr_pred splits batches of at least this many trees into 2 stream groups
 PRED_GROUP_MIN = int(os.environ.get("CIT_PRED_GROUP_MIN", "2048"))
-PRED_GROUPS = int(os.environ.get("CIT_PRED_GROUPS", "3"))   # 1 / 2 / 3 / 4: 87.0k / 96.9k / 100.3k / 61.4k decisions/s (config 4, profiles/r03/pred_groups)
+PRED_GROUPS = int(os.environ.get("CIT_PRED_GROUPS", "3"))
+# cfr_pred time slices (cit_cfr_pred_slice), 100 MHz GPU wall-clock ticks per
+# search launch; 0 = a launch runs every tree to its next leaf (cit_cfr_pred_step)
+PRED_SLICE_TICKS = int(os.environ.get("CIT_PRED_SLICE_TICKS", "0"))   # 1 / 2 / 3 / 4: 87.0k / 96.9k / 100.3k / 61.4k decisions/s (config 4, profiles/r03/pred_groups)
 _side_streams = {}
 
 
@@ -455,7 +459,7 @@ class GameBatch:
         return (int(h[0]), int(h[2])), (int(h[1]), int(h[3]))
 
     def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000, max_retries=3,
-                 flags=0, orig=None, groups="auto"):
+                 flags=0, orig=None, groups="auto", slice_ticks="auto"):
         """run_mccfr(game, model, max_iterations=iters) with a model and training=False
         (cfr_pred(iters, max_depth) + live action choice) on every lane.  `net` is a
         models.ValueNet; leaf rows of all suspended trees are evaluated in one MFMA
@@ -466,7 +470,12 @@ class GameBatch:
         sub-batches whose rounds run on their own HIP streams, interleaved, so
         one group's search kernel fills the SIMDs while another waits for its
         leaf evaluation and the host's round turnaround (a round lasts as long
-        as its slowest tree); every tree is searched exactly as in one batch."""
+        as its slowest tree); every tree is searched exactly as in one batch.
+        slice_ticks > 0 (auto: PRED_SLICE_TICKS): each search launch also
+        stops a tree at an iteration boundary after that much GPU wall clock,
+        so a round ends with the slice rather than its slowest tree; results
+        are the same."""
+        self._slice_ticks = PRED_SLICE_TICKS if slice_ticks == "auto" else int(slice_ticks)
         if not hasattr(self, "np_mt"):
             self.seed_numpy()
         snap = self._snapshot() if max_retries > 0 else None
@@ -480,7 +489,8 @@ class GameBatch:
         box = [rounds]
 
         def run(sub, nc, ec, mr, o):
-            c, st, r = sub.cfr_pred(iters, net, max_depth, nc, ec, max_rounds, mr, flags, o)
+            c, st, r = sub.cfr_pred(iters, net, max_depth, nc, ec, max_rounds, mr, flags, o,
+                                    slice_ticks=self._slice_ticks)
             box[0] += r
             return c, st
         chosen, stats = self._retry_overflow(snap, stats, chosen, run, max_retries, orig)
@@ -496,23 +506,28 @@ class GameBatch:
                       "feat": torch.zeros((self.B, 418), dtype=torch.float32, device=d),
                       "probs": torch.zeros((self.B, 6), dtype=torch.float32, device=d),
                       "chosen": torch.zeros((self.B, 16), dtype=torch.uint8, device=d),
-                      "waiting": torch.zeros(1, dtype=torch.int32, device=d)}
+                      "waiting": torch.zeros(2, dtype=torch.int32, device=d),     # waiting, running
+                      "ticks": getattr(self, "_slice_ticks", 0)}
 
     def _pred_step(self, iters, max_depth, flags):
         """One cit_cfr_pred_step launch (every tree runs to its next leaf evaluation or its end)."""
         P = self._pred
         o = P["o"]
         P["waiting"].zero_()
-        _lib.check(self.lib.cit_cfr_pred_step(
+        w = _ptr(P["waiting"])
+        _lib.check(self.lib.cit_cfr_pred_slice(
             _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
             _ptr(self.seer), self.B, int(iters), int(flags), None if o is None else _ptr(o), int(max_depth),
             _ptr(self.pool), self.node_cap, self.edge_cap, _ptr(self.optbuf), _ptr(P["state"]), _ptr(P["probs"]),
-            _ptr(P["feat"]), _ptr(P["chosen"]), _ptr(P["waiting"]), _stream()), "cit_cfr_pred_step")
+            _ptr(P["feat"]), _ptr(P["chosen"]), int(P["ticks"]), w, w + 4, _stream()), "cit_cfr_pred_slice")
 
     def _pred_leaves(self, net):
         P = self._pred
-        _lib.check(self.lib.cit_mlp_forward(_ptr(P["feat"]), self.B, *[t.data_ptr() for t in net.w], _ptr(P["probs"]),
-                                            None, _stream()), "cit_mlp_forward")
+        if P.get("work") is None:
+            P["work"] = net.workspace(self.B)
+        _lib.check(self.lib.cit_mlp_forward_packed(_ptr(P["feat"]), self.B, net.packed.data_ptr(), _ptr(P["probs"]),
+                                                   None, _ptr(P["work"]), P["work"].numel(), _stream()),
+                   "cit_mlp_forward_packed")
 
     def _pred_end(self):
         P = self._pred
@@ -525,10 +540,12 @@ class GameBatch:
         rounds = 0
         while rounds < max_rounds:
             self._pred_step(iters, max_depth, flags)
-            if int(self._pred["waiting"].item()) == 0:
+            waiting, running = self._pred["waiting"].tolist()
+            if waiting == 0 and running == 0:
                 break
-            self._pred_leaves(net)
-            rounds += 1
+            if waiting:
+                self._pred_leaves(net)
+                rounds += 1
         chosen, stats = self._pred_end()
         return chosen, stats, rounds
 
@@ -540,6 +557,7 @@ class GameBatch:
         subs, streams = [], []
         for g, lanes in enumerate(parts):
             sub = self.subset(lanes)
+            sub._slice_ticks = getattr(self, "_slice_ticks", 0)
             st = side_streams(self.device, G)[g]
             st.wait_stream(cur)
             with torch.cuda.stream(st):
@@ -553,11 +571,13 @@ class GameBatch:
             for g in list(active):
                 sub = subs[g]
                 with torch.cuda.stream(streams[g]):
-                    if int(sub._pred["waiting"].item()) == 0 or rounds[g] >= max_rounds:
+                    waiting, running = sub._pred["waiting"].tolist()
+                    if (waiting == 0 and running == 0) or rounds[g] >= max_rounds:
                         active.remove(g)
                         continue
-                    sub._pred_leaves(net)
-                    rounds[g] += 1
+                    if waiting:
+                        sub._pred_leaves(net)
+                        rounds[g] += 1
                     sub._pred_step(iters, max_depth, flags)
         chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
         stats = torch.zeros((self.B, 5), dtype=torch.int32)

@@ -3,7 +3,7 @@ ValueOnlyNN(418, hidden) = fc1 -> BN -> ReLU -> Dropout(0.2) -> fc2 -> BN ->
 ReLU -> Dropout -> fc3 -> ReLU -> fc4 (6 logits).  Same parameter names, so a
 reference state_dict loads unchanged.  `ValueNet` is its inference form on
 the MI355X: BatchNorm folded into fc1/fc2 (eval mode), weights transposed to
-[in][out] and resident in HBM, forward = the fp32-MFMA kernel cit_mlp_forward
+[in][out] and resident in HBM, forward = the fp32-MFMA kernels of cit_mlp_forward_packed
 (+ square_and_normalize, train_utils.py:143-145)."""
 import torch
 import torch.nn as nn
@@ -64,14 +64,32 @@ class ValueNet:
         self.device = torch.device(device)
         self.host = fold(model)
         self.w = [t.to(self.device) for t in self.host]
+        self.packed = torch.empty(int(self.lib.cit_mlp_packed_bytes()), dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.cit_mlp_pack(*[t.data_ptr() for t in self.w], self.packed.data_ptr(),
+                                         torch.cuda.current_stream(self.device).cuda_stream), "cit_mlp_pack")
 
-    def forward(self, feat, logits=False):
+    def forward(self, feat, logits=False, fused=False):
+        """probs [M][6] (and logits).  Default: the layer-split launches over
+        the packed weights (cit_mlp_forward_packed, H1 / H2 in a workspace
+        from torch's caching allocator); fused=True: the one-launch k_mlp
+        (cit_mlp_forward).  Both give bitwise the same outputs."""
         feat = feat.contiguous()
         M = feat.shape[0]
         probs = torch.empty((M, 6), dtype=torch.float32, device=self.device)
         lg = torch.empty((M, 6), dtype=torch.float32, device=self.device) if logits else None
-        ptrs = [t.data_ptr() for t in self.w]
-        _lib.check(self.lib.cit_mlp_forward(feat.data_ptr(), M, *ptrs, probs.data_ptr(),
-                                            lg.data_ptr() if lg is not None else None,
-                                            torch.cuda.current_stream().cuda_stream), "cit_mlp_forward")
+        s = torch.cuda.current_stream().cuda_stream
+        if fused:
+            ptrs = [t.data_ptr() for t in self.w]
+            _lib.check(self.lib.cit_mlp_forward(feat.data_ptr(), M, *ptrs, probs.data_ptr(),
+                                                lg.data_ptr() if lg is not None else None, s), "cit_mlp_forward")
+        else:
+            work = self.workspace(M)
+            _lib.check(self.lib.cit_mlp_forward_packed(feat.data_ptr(), M, self.packed.data_ptr(), probs.data_ptr(),
+                                                       lg.data_ptr() if lg is not None else None, work.data_ptr(),
+                                                       work.numel(), s), "cit_mlp_forward_packed")
         return (probs, lg) if logits else probs
+
+    def workspace(self, M):
+        """A device buffer for cit_mlp_forward_packed over M rows (stream-ordered
+        by torch's caching allocator)."""
+        return torch.empty(max(int(self.lib.cit_mlp_work_bytes(M)), 16), dtype=torch.uint8, device=self.device)

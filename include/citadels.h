@@ -48,7 +48,7 @@ typedef struct CitOption {
   uint64_t x;
 } CitOption;
 
-int cit_abi_version(void);              /* 4: node pools with diff row slots (cit_cfr_arena_reset_rows) */
+int cit_abi_version(void);              /* 5: packed value-MLP path (4: node pools with diff row slots) */
 int cit_game_bytes(void);              /* row width of `games` */
 int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
 int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
@@ -145,6 +145,19 @@ int cit_encode_options(const void* games, const CitOption* opts, const int32_t* 
 int cit_mlp_forward(const float* feat, int M, const float* w1t, const float* b1, const float* w2t, const float* b2,
                     const float* w3t, const float* b3, const float* w4t, const float* b4, float* probs, float* logits,
                     hipStream_t stream);
+/* The same forward, bitwise equal, as three launches that spread fc1 and
+ * fc2 over one workgroup per row tile x column group (a 1,024-row leaf
+ * batch fills the chip instead of 64 CUs).  The weights are first packed
+ * once by cit_mlp_pack into `packed` (cit_mlp_packed_bytes() bytes of device
+ * memory, the MFMA operand order plus the biases); H1 / H2 go through
+ * `work`, at least cit_mlp_work_bytes(M) bytes the call owns until it
+ * completes on `stream`. */
+size_t cit_mlp_packed_bytes(void);
+int cit_mlp_pack(const float* w1t, const float* b1, const float* w2t, const float* b2, const float* w3t,
+                 const float* b3, const float* w4t, const float* b4, void* packed, hipStream_t stream);
+size_t cit_mlp_work_bytes(int M);
+int cit_mlp_forward_packed(const float* feat, int M, const void* packed, float* probs, float* logits, void* work,
+                           size_t work_bytes, hipStream_t stream);
 
 /* --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------ */
 
@@ -200,6 +213,11 @@ int cit_advance_random(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
  * `orig_player` [B] = CFRNode's original_player_id per lane, or NULL for the
  * game's current player before the root's skip_false_choice (run_mccfr). */
 #define CIT_CFR_ROOT_SKIPPED 1
+/* CIT_CFR_STRATEGY_HBM (a checking aid): update_strategy keeps no LDS copy of
+ * S / CS and runs over the edge records in HBM for every node (the path the
+ * kernels take for nodes with more than 96 children); the trees are bitwise
+ * the same. */
+#define CIT_CFR_STRATEGY_HBM 2
 
 /* CFRNode.skip_false_choice() (algorithms/deep_mccfr.py:37-49) on every lane,
  * as the CFRNode constructor runs it on the game it is given (:19-20):
@@ -246,7 +264,7 @@ int cit_cfr_arena_release(void* pool, int B, int node_cap, int edge_cap, const i
  * before the first call.  Each call advances every unfinished tree until it
  * needs its next leaf evaluation (that node's encode_game row goes to
  * feat[l][418] and *waiting is incremented) or finishes (chosen[l], games[l] =
- * root game).  Between calls evaluate feat with cit_mlp_forward into
+ * root game).  Between calls evaluate feat with cit_mlp_forward or cit_mlp_forward_packed into
  * probs[l][6]; stop when a call leaves *waiting == 0.  Leaves are evaluated
  * once per node (the reference recomputes the same value). */
 int cit_cfr_state_bytes(void);
@@ -254,6 +272,18 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
                       int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,
                       int node_cap, int edge_cap, CitOption* optbuf, void* state, const float* probs, float* feat,
                       CitOption* chosen, int32_t* waiting, hipStream_t stream);
+/* cit_cfr_pred_step with a time slice: a tree also stops, at an iteration
+ * boundary, once slice_ticks of the 100 MHz GPU wall clock have passed since
+ * the launch reached it (then *running is incremented; 0 = no limit, as
+ * cit_cfr_pred_step).  Call again while *waiting or *running is non-zero,
+ * evaluating feat first when *waiting is; the trees, streams and counters
+ * are bit-identical to cit_cfr_pred_step's rounds.  A round then ends with a
+ * slice instead of with its slowest tree. */
+int cit_cfr_pred_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                       int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,
+                       int node_cap, int edge_cap, CitOption* optbuf, void* state, const float* probs, float* feat,
+                       CitOption* chosen, int64_t slice_ticks, int32_t* waiting, int32_t* running,
+                       hipStream_t stream);
 
 /* compare_to_random.play_games' step loop (compare_to_random.py:16-35) on
  * every lane up to its next searched decision: seats in search_mask (bit p =

@@ -13,7 +13,7 @@ import torch
 from citadels_self_play_amd import canon
 from citadels_self_play_amd import layout as L
 from conftest import load_golden
-from test_cfr_host_golden import compare_node, dfs, hash_obj
+from test_cfr_host_golden import arrays, compare_node, dfs, hash_obj
 
 pytestmark = pytest.mark.gpu
 
@@ -112,6 +112,37 @@ def test_gpu_cfr_batch_properties():
     c2, s2 = small.cfr_decide(200)
     assert np.array_equal(c2.cpu().numpy(), out[0][0][::97])
     assert np.array_equal(s2.cpu().numpy()[:, 1:], out[0][1][::97, 1:])
+
+
+def test_gpu_cfr_strategy_lds_equals_hbm_path():
+    """update_strategy's LDS copies (nodes of <= 96 children) and its HBM
+    path (larger nodes; forced for every node by CIT_CFR_STRATEGY_HBM) build
+    bitwise the same trees: every node and edge record, decisions, streams."""
+    from citadels_self_play_amd.engine import CFR_STRATEGY_HBM
+    seeds = np.arange(9_100_000, 9_100_000 + 64)
+    res = []
+    for flags in (0, CFR_STRATEGY_HBM):
+        b = _batch(seeds)
+        b.advance_random(0, 300)
+        b.seed_numpy()
+        chosen, stats = b.cfr_decide(2000, node_cap=8192, edge_cap=5 * 8192, flags=flags)
+        trees = [b.tree(l)[:2] for l in range(len(seeds))]
+        res.append((chosen.cpu().numpy(), stats.cpu().numpy(), b.rows(), b.mt.cpu().numpy(),
+                    b.np_mt.cpu().numpy(), b.np_idx.cpu().numpy(), trees))
+    a, h = res
+    for x, y in zip(a[:6], h[:6]):
+        assert np.array_equal(x, y)
+    for l, ((na, ea), (nh, eh)) in enumerate(zip(a[6], h[6])):
+        n = int(a[1][l][1])
+        for f in na.dtype.names:
+            if f != "pad":
+                assert np.ascontiguousarray(na[f][:n]).tobytes() == np.ascontiguousarray(nh[f][:n]).tobytes(), (l, f)
+        for i in range(n):                       # the written edge records of every node (reserved slots aside)
+            assert repr(arrays(na, ea, i)) == repr(arrays(nh, eh, i)), (l, i)
+            fe, nch = int(na[i]["first_edge"]), int(na[i]["n_children"])
+            if nch:
+                assert ea[fe:fe + nch]["opt"].tobytes() == eh[fe:fe + nch]["opt"].tobytes(), (l, i)
+                assert ea[fe:fe + nch]["child"].tobytes() == eh[fe:fe + nch]["child"].tobytes(), (l, i)
 
 
 def test_gpu_cfr_streams_overlap():

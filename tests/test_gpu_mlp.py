@@ -33,18 +33,51 @@ def golden():
     return g
 
 
+@pytest.mark.parametrize("fused", [False, True], ids=["layers", "fused"])
 @pytest.mark.parametrize("variant", ["init", "bn"])
-def test_gpu_mlp_bitwise_vs_fma_oracle(golden, variant):
+def test_gpu_mlp_bitwise_vs_fma_oracle(golden, variant, fused):
     m = load_variant(golden, variant)
     net = models.ValueNet(m, "cuda")
     x = np.concatenate([golden["x"], golden["x"][:45] * 0.5])      # ragged last tile (301 rows)
-    probs, logits = net.forward(torch.from_numpy(x).cuda(), logits=True)
+    probs, logits = net.forward(torch.from_numpy(x).cuda(), logits=True, fused=fused)
     probs, logits = probs.cpu().numpy(), logits.cpu().numpy()
     fp, fl = M.FmaMLP(models.fold(m))(x, logits=True)
     assert np.array_equal(logits.view(np.uint32), fl.view(np.uint32))
     assert np.array_equal(probs.view(np.uint32), fp.view(np.uint32))
     np.testing.assert_allclose(probs[:256], golden["%s.probs" % variant], rtol=PROB_RTOL * 50, atol=PROB_ATOL * 10)
     np.testing.assert_allclose(logits[:256], golden["%s.logits" % variant], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("rows", [1, 16, 17, 1024, 1029])
+def test_gpu_mlp_layer_split_equals_fused(golden, rows):
+    """cit_mlp_forward_packed (fc1 / fc2 spread over the chip) and the one-launch
+    k_mlp give bitwise the same probs / logits at every row count, including
+    a single row and ragged last tiles; the first rows also equal the oracle."""
+    net = models.ValueNet(load_variant(golden, "bn"), "cuda")
+    g = torch.Generator().manual_seed(rows)
+    x = torch.randint(-3, 6, (rows, 418), generator=g).float() * 0.25
+    x[: min(rows, 64)] = torch.from_numpy(golden["x"][: min(rows, 64)])
+    pa, la = net.forward(x.cuda(), logits=True)
+    pb, lb = net.forward(x.cuda(), logits=True, fused=True)
+    assert torch.equal(pa.view(torch.int32), pb.view(torch.int32))
+    assert torch.equal(la.view(torch.int32), lb.view(torch.int32))
+    k = min(rows, 40)
+    fp, fl = M.FmaMLP(models.fold(load_variant(golden, "bn")))(x[:k].numpy(), logits=True)
+    assert np.array_equal(la[:k].cpu().numpy().view(np.uint32), fl.view(np.uint32))
+    assert np.array_equal(pa[:k].cpu().numpy().view(np.uint32), fp.view(np.uint32))
+
+
+def test_gpu_mlp_packed_rejects_short_workspace(golden):
+    from citadels_self_play_amd import _lib
+    net = models.ValueNet(load_variant(golden, "init"), "cuda")
+    lib = _lib.load()
+    x = torch.zeros((40, 418), device="cuda")
+    probs = torch.zeros((40, 6), device="cuda")
+    need = int(lib.cit_mlp_work_bytes(40))
+    assert need == 40 * (512 + 256) * 4
+    work = torch.empty(need - 4, dtype=torch.uint8, device="cuda")
+    assert lib.cit_mlp_forward_packed(x.data_ptr(), 40, net.packed.data_ptr(), probs.data_ptr(), None,
+                                      work.data_ptr(), need - 4, None) == -1
 
 
 def test_gpu_encode_matches_host():

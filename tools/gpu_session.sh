@@ -18,6 +18,7 @@
 #   ab=LIBS          tools/_ablib.py A/B of rollout builds (colon-separated .so
 #                    paths), 3 interleaved reps each           -> ab/summary.txt
 #   py=SCRIPT[:ARGS] python SCRIPT ARGS                          -> py_<n>.log
+#   pyprof=SCRIPT[:ARGS] the same under rocprofv3 --kernel-trace --stats -> pyprof_<n>/
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -74,6 +75,11 @@ run_step() {
       local script=${val%%:*} args=
       [[ $val == *:* ]] && args=${val#*:}
       (cd "$R" && timeout -k 10 900 python -u "$script" ${args//,/ } > "$O/py_$n.log" 2>&1) ;;
+    pyprof)
+      local script=${val%%:*} args=
+      [[ $val == *:* ]] && args=${val#*:}
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pyprof_$n" -o run -- \
+        python3 "$R/$script" ${args//,/ } > "$O/pyprof_$n.log" 2>&1) ;;
     *)
       echo "unknown step $step" >&2
       return 2 ;;

@@ -72,6 +72,12 @@ PRED_GROUP_MIN = int(os.environ.get("CIT_PRED_GROUP_MIN", "2048"))
 PRED_GROUPS = int(os.environ.get("CIT_PRED_GROUPS", "3"))
 # cfr_pred time slices (cit_cfr_pred_slice), 100 MHz GPU wall-clock ticks per
 # search launch; 0 = a launch runs every tree to its next leaf (cit_cfr_pred_step)
+# cfr_pred rounds enqueued per host poll: a search launch, the leaf evaluation,
+# the next launch, ... without reading the waiting counters in between (each
+# round counts into its own slot, read once per batch), so a group's stream
+# never idles for the host's round turnaround; launches past the end find
+# every tree done and return at once
+PRED_AHEAD = int(os.environ.get("CIT_PRED_AHEAD", "1"))
 PRED_SLICE_TICKS = int(os.environ.get("CIT_PRED_SLICE_TICKS", "0"))   # 1 / 2 / 3 / 4: 87.0k / 96.9k / 100.3k / 61.4k decisions/s (config 4, profiles/r03/pred_groups)
 _side_streams = {}
 
@@ -506,15 +512,16 @@ class GameBatch:
                       "feat": torch.zeros((self.B, 418), dtype=torch.float32, device=d),
                       "probs": torch.zeros((self.B, 6), dtype=torch.float32, device=d),
                       "chosen": torch.zeros((self.B, 16), dtype=torch.uint8, device=d),
-                      "waiting": torch.zeros(2, dtype=torch.int32, device=d),     # waiting, running
-                      "ticks": getattr(self, "_slice_ticks", 0)}
+                      "waiting": torch.zeros((max(1, PRED_AHEAD), 2), dtype=torch.int32, device=d),
+                      "ticks": getattr(self, "_slice_ticks", 0)}       # (waiting, running) per round of a batch
 
-    def _pred_step(self, iters, max_depth, flags):
-        """One cit_cfr_pred_step launch (every tree runs to its next leaf evaluation or its end)."""
+    def _pred_step(self, iters, max_depth, flags, slot=0):
+        """One cit_cfr_pred_step launch (every tree runs to its next leaf evaluation
+        or its end); its waiting / running counts go to round slot `slot` (zeroed
+        by the caller)."""
         P = self._pred
         o = P["o"]
-        P["waiting"].zero_()
-        w = _ptr(P["waiting"])
+        w = _ptr(P["waiting"]) + 8 * slot
         _lib.check(self.lib.cit_cfr_pred_slice(
             _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
             _ptr(self.seer), self.B, int(iters), int(flags), None if o is None else _ptr(o), int(max_depth),
@@ -535,17 +542,42 @@ class GameBatch:
         stats = torch.stack([st[:, 8], st[:, 0], st[:, 1], st[:, 3], st[:, 2]], dim=1)
         return P["chosen"], stats
 
+    def _pred_batch(self, net, iters, max_depth, flags, lead, n):
+        """Enqueue n rounds (PRED_AHEAD): search launch j counts into slot j, and
+        a leaf evaluation runs between launches (and first when `lead`: the
+        previous batch's last launch left trees waiting).  A leaf evaluation
+        with no tree waiting rewrites the same probabilities, and a launch
+        after every tree is done returns at once, so the trees are searched
+        exactly as with a host check after every launch."""
+        self._pred["waiting"].zero_()
+        for j in range(n):
+            if j or lead:
+                self._pred_leaves(net)
+            self._pred_step(iters, max_depth, flags, j)
+
+    def _pred_poll(self, n):
+        """(done, leaf rounds, lead) from the slots of the last batch of n rounds:
+        the rounds whose launch left trees waiting, up to the first launch
+        after which no tree waits or runs."""
+        rounds = 0
+        cnt = self._pred["waiting"][:n].tolist()
+        for waiting, running in cnt:
+            if waiting == 0 and running == 0:
+                return True, rounds, False
+            rounds += waiting > 0
+        return False, rounds, cnt[-1][0] > 0
+
     def _cfr_pred(self, iters, net, max_depth, node_cap, edge_cap, max_rounds, flags=0, orig=None):
         self._pred_begin(node_cap, edge_cap, orig)
-        rounds = 0
+        A = self._pred["waiting"].shape[0]
+        rounds, lead = 0, False
         while rounds < max_rounds:
-            self._pred_step(iters, max_depth, flags)
-            waiting, running = self._pred["waiting"].tolist()
-            if waiting == 0 and running == 0:
+            n = max(1, min(A, max_rounds - rounds))
+            self._pred_batch(net, iters, max_depth, flags, lead, n)
+            done, r, lead = self._pred_poll(n)
+            rounds += r
+            if done:
                 break
-            if waiting:
-                self._pred_leaves(net)
-                rounds += 1
         chosen, stats = self._pred_end()
         return chosen, stats, rounds
 
@@ -562,23 +594,24 @@ class GameBatch:
             st.wait_stream(cur)
             with torch.cuda.stream(st):
                 sub._pred_begin(node_cap, edge_cap, None if o is None else o[lanes.cpu().numpy()])
-                sub._pred_step(iters, max_depth, flags)
+                n0 = max(1, min(sub._pred["waiting"].shape[0], max_rounds))
+                sub._pred_batch(net, iters, max_depth, flags, False, n0)
             subs.append(sub)
             streams.append(st)
         rounds = [0] * G
+        last = [n0] * G
         active = list(range(G))
         while active:
             for g in list(active):
                 sub = subs[g]
                 with torch.cuda.stream(streams[g]):
-                    waiting, running = sub._pred["waiting"].tolist()
-                    if (waiting == 0 and running == 0) or rounds[g] >= max_rounds:
+                    done, r, lead = sub._pred_poll(last[g])
+                    rounds[g] += r
+                    if done or rounds[g] >= max_rounds:
                         active.remove(g)
                         continue
-                    if waiting:
-                        sub._pred_leaves(net)
-                        rounds[g] += 1
-                    sub._pred_step(iters, max_depth, flags)
+                    last[g] = max(1, min(sub._pred["waiting"].shape[0], max_rounds - rounds[g]))
+                    sub._pred_batch(net, iters, max_depth, flags, lead, last[g])
         chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
         stats = torch.zeros((self.B, 5), dtype=torch.int32)
         for g, (sub, lanes) in enumerate(zip(subs, parts)):

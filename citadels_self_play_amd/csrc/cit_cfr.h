@@ -261,22 +261,28 @@ struct CfrLds {
   CfrState S;
   int cnode, cnch;                                // node (and its child count) whose normalised CS is in cbuf (-1: none)
   int sbuf_on;                                    // 0 under CIT_CFR_STRATEGY_HBM
+  int base_off;                                   // dwords from cfr_dyn to the base row (diff-row pools)
   // cit_sample_private's scratch is read and written 16 bytes at a time:
   // keep it 16-byte aligned whatever the fields above add up to
   __attribute__((aligned(16))) uint8_t tmp[CIT_SAMPLE_SCRATCH];
 };
 static __shared__ __attribute__((aligned(16))) CfrLds cfr_ls;
 // Dynamic LDS of a search launch (sized per launch, cfr_dyn_lds_bytes): the
-// tree's base row (diff row slots), then its two block tables interleaved
-// (node-block entry i at [2i], edge-block entry i at [2i + 1]) so both start
-// at fixed addresses whatever the capacities; a tree's tables hold
-// max(nblocks, eblocks) entries each (2 at configs 3/4, 172 at
-// cfr_train(200000)) instead of a fixed CFR_TBL_MAX.
+// tree's two block tables interleaved (node-block entry i at [2i], edge-block
+// entry i at [2i + 1]) so both start at a fixed address whatever the
+// capacities; a tree's tables hold max(nblocks, eblocks) entries each (2 at
+// configs 3/4, 172 at cfr_train(200000)) instead of a fixed CFR_TBL_MAX.
+// Then, for a pool with diff row slots only, the tree's base row at
+// cfr_dyn_base_off dwords (CfrLds.base_off): a raw-row launch (configs 3/4)
+// takes 16 B of dynamic LDS instead of 1.6 KB.
 extern __shared__ __attribute__((aligned(16))) uint32_t cfr_dyn[];
 #endif
-CIT_HD int64_t cfr_dyn_lds_bytes(int node_cap, int edge_cap) {
+CIT_HD int64_t cfr_dyn_base_off(int node_cap, int edge_cap) {
   int nb = cfr_nblocks(node_cap), eb = cfr_eblocks(edge_cap);
-  return 4 * ((int64_t)CFR_ROW_W + 2 * (int64_t)(nb > eb ? nb : eb));
+  return (2 * (int64_t)(nb > eb ? nb : eb) + 3) & ~(int64_t)3;      // 16-byte aligned: rows move as 16-B words
+}
+CIT_HD int64_t cfr_dyn_lds_bytes(int node_cap, int edge_cap, bool base_row) {
+  return 4 * (cfr_dyn_base_off(node_cap, edge_cap) + (base_row ? (int64_t)CFR_ROW_W : 0));
 }
 #if CIT_WAVE
 #define CFR_T(T_in) (cfr_ls.T)
@@ -331,13 +337,17 @@ CIT_HD int cfr_take_block(CfrArena* A, int edge) {
 // the pool's.  Entry i of the node- / edge-block table.
 #if CIT_WAVE
 __device__ __forceinline__ int32_t& cfr_nbt_at(const CfrTree&, int i) {
-  return reinterpret_cast<int32_t*>(cfr_dyn + CFR_ROW_W)[2 * i];
+  return reinterpret_cast<int32_t*>(cfr_dyn)[2 * i];
 }
 __device__ __forceinline__ int32_t& cfr_ebt_at(const CfrTree&, int i) {
-  return reinterpret_cast<int32_t*>(cfr_dyn + CFR_ROW_W)[2 * i + 1];
+  return reinterpret_cast<int32_t*>(cfr_dyn)[2 * i + 1];
 }
-__device__ __forceinline__ const uint32_t* cfr_base(const CfrTree&) { return cfr_dyn; }
-__device__ __forceinline__ uint32_t* cfr_base_w(const CfrTree&) { return cfr_dyn; }
+__device__ __forceinline__ const uint32_t* cfr_base(const CfrTree&) {
+  return cfr_dyn + __builtin_amdgcn_readfirstlane(cfr_ls.base_off);
+}
+__device__ __forceinline__ uint32_t* cfr_base_w(const CfrTree&) {
+  return cfr_dyn + __builtin_amdgcn_readfirstlane(cfr_ls.base_off);
+}
 #else
 CIT_HD int32_t& cfr_nbt_at(const CfrTree& T, int i) { return T.nbt[i]; }
 CIT_HD int32_t& cfr_ebt_at(const CfrTree& T, int i) { return T.ebt[i]; }

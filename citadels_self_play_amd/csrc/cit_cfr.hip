@@ -4,6 +4,9 @@
 #define CIT_MT_COOP_ONLY 1
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "../../include/citadels.h"
 #include "cit_cfr.h"
 
@@ -41,9 +44,10 @@ __device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, 
 // streams, working rows.
 __device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx,
                                            uint64_t* seer, int B, long l, uint8_t* pool, int node_cap, int edge_cap,
-                                           CitOpt* optbuf, int flags) {
+                                           CitOpt* optbuf, int flags, int base_off) {
   CfrTree& T = cfr_ls.T;
   cfr_ls.cnode = -1;
+  cfr_ls.base_off = base_off;
   cfr_ls.sbuf_on = (flags & CIT_CFR_STRATEGY_HBM) ? 0 : 1;
   cfr_tree_bind(T, pool, B, l, node_cap, edge_cap);
   T.nbt = nullptr;          // the tables live in dynamic LDS (cfr_nbt_at / cfr_ebt_at)
@@ -67,7 +71,7 @@ __device__ __forceinline__ void tables_load(const CfrTree& T, int n_nodes, int n
   for (int i = threadIdx.x; i < nb; i += blockDim.x) cfr_nbt_at(T, i) = T.nbt_hbm[i];
   for (int i = threadIdx.x; i < eb; i += blockDim.x) cfr_ebt_at(T, i) = T.ebt_hbm[i];
   if (T.row_cap)
-    for (int i = threadIdx.x; i < CFR_ROW_W; i += blockDim.x) cfr_dyn[i] = T.base_hbm[i];
+    for (int i = threadIdx.x; i < CFR_ROW_W; i += blockDim.x) cfr_base_w(T)[i] = T.base_hbm[i];
   __syncthreads();
 }
 __device__ __forceinline__ void tables_store(const CfrTree& T) {
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_decide(uint32_t* games, uint
                                                    uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
                                                    const int32_t* orig, uint8_t* pool,
                                                    int node_cap, int edge_cap, CitOpt* optbuf, CitOpt* chosen,
-                                                   int32_t* stats) {
+                                                   int32_t* stats, int base_off) {
   long l = blockIdx.x;
   if (l >= B) return;
 #ifdef CFR_TREE_CLOCK
@@ -105,7 +109,7 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_decide(uint32_t* games, uint
 #endif
   cfr_prof_reset();
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags);
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off);
   T.n_nodes = T.n_edges = 0;
   T.err = 0;
   T.carry_outs = 0;
@@ -145,7 +149,7 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_pred_step(uint32_t* games, u
                                                       const int32_t* orig, int max_depth, uint8_t* pool, int node_cap, int edge_cap, CitOpt* optbuf,
                                                       CfrState* state, const float* probs, float* feat,
                                                       CitOpt* chosen, int32_t* waiting, uint64_t ticks,
-                                                      int32_t* running) {
+                                                      int32_t* running, int base_off) {
   long l = blockIdx.x;
   if (l >= B) return;
   CfrBudget bud;
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_pred_step(uint32_t* games, u
   S = state[l];             // every lane stores the same value
   if (S.phase == CP_DONE) return;
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags);
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off);
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;
@@ -194,7 +198,8 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_train_slice(uint32_t* games,
                                                         uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
                                                         const int32_t* orig, uint8_t* pool, int node_cap, int edge_cap,
                                                         CitOpt* optbuf, CfrState* state, uint64_t ticks,
-                                                        CitOpt* chosen, int32_t* stats, int32_t* running) {
+                                                        CitOpt* chosen, int32_t* stats, int32_t* running,
+                                                        int base_off) {
   long l = blockIdx.x;
   if (l >= B) return;
   CfrBudget bud;
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_train_slice(uint32_t* games,
   S = state[l];
   if (S.phase == CP_DONE) return;
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags);
+  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off);
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;
@@ -285,6 +290,30 @@ __global__ void k_arena_reset(int32_t* pool, long per_words, long tbl_words, int
         threadIdx.x == 1 ? n_cap : threadIdx.x == 3 ? e_cap : threadIdx.x == 8 ? row_cap : 0u;
 }
 
+// Row slot format of each pool this library reset (cit_cfr_arena_reset_rows),
+// so a search launch reserves dynamic LDS for the base row only when the pool
+// stores diff rows; a pool not reset here gets the room (diff rows or not).
+std::mutex g_pool_rows_mu;
+std::unordered_map<const void*, int> g_pool_rows;
+void pool_rows_set(const void* pool, int row_cap) {
+  std::lock_guard<std::mutex> lk(g_pool_rows_mu);
+  g_pool_rows[pool] = row_cap;
+}
+struct DynLds {
+  size_t bytes;
+  int base_off;     // dwords from cfr_dyn to the base row; -1: no room (raw rows)
+};
+DynLds dyn_lds(const void* pool, int node_cap, int edge_cap) {
+  bool base = true;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_rows_mu);
+    auto it = g_pool_rows.find(pool);
+    if (it != g_pool_rows.end()) base = it->second != 0;
+  }
+  return {(size_t)cfr_dyn_lds_bytes(node_cap, edge_cap, base),
+          base ? (int)cfr_dyn_base_off(node_cap, edge_cap) : -1};
+}
+
 }  // namespace
 
 #define CHECK_LAUNCH()                       \
@@ -320,6 +349,7 @@ int cit_cfr_arena_reset_rows(void* pool, int B, int node_cap, int edge_cap, int 
   if (!pool || B <= 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || node_blocks < 0 || edge_blocks < 0 ||
       !cfr_row_cap_ok(row_cap))
     return -1;
+  pool_rows_set(pool, row_cap);
   long per_words = (long)(cfr_pool_bytes(node_cap, edge_cap) / 4);
   long tbl_words = (long)(cfr_tables_bytes(node_cap, edge_cap) / 4);
   uint8_t* a = (uint8_t*)pool + per_words * 4 * B;
@@ -352,8 +382,10 @@ int cit_cfr_decide(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt,
   if (B <= 0 || iters < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt || !mt_idx || !np_mt ||
       !np_idx || !seer || !pool || !optbuf || !chosen || !stats)
     return -1;
-  hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
-                     B, iters, flags, orig_player, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats);
+  DynLds d = dyn_lds(pool, node_cap, edge_cap);
+  hipLaunchKernelGGL(k_cfr_decide, dim3(B), dim3(64), d.bytes, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer,
+                     B, iters, flags, orig_player, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CitOpt*)chosen, stats,
+                     d.base_off);
   CHECK_LAUNCH();
 }
 
@@ -366,9 +398,10 @@ int cit_cfr_train_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* n
   if (B <= 0 || iters < 0 || slice_ticks < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt ||
       !mt_idx || !np_mt || !np_idx || !seer || !pool || !optbuf || !state || !chosen || !stats || !running)
     return -1;
-  hipLaunchKernelGGL(k_cfr_train_slice, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
+  DynLds d = dyn_lds(pool, node_cap, edge_cap);
+  hipLaunchKernelGGL(k_cfr_train_slice, dim3(B), dim3(64), d.bytes, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
                      seer, B, iters, flags, orig_player, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
-                     (CfrState*)state, (uint64_t)slice_ticks, (CitOpt*)chosen, stats, running);
+                     (CfrState*)state, (uint64_t)slice_ticks, (CitOpt*)chosen, stats, running, d.base_off);
   CHECK_LAUNCH();
 }
 
@@ -379,9 +412,10 @@ int cit_cfr_pred_step(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_
   if (B <= 0 || iters < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt || !mt_idx || !np_mt ||
       !np_idx || !seer || !pool || !optbuf || !state || !probs || !feat || !chosen || !waiting)
     return -1;
-  hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
+  DynLds d = dyn_lds(pool, node_cap, edge_cap);
+  hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), d.bytes, stream, (uint32_t*)games, mt, mt_idx, np_mt, np_idx,
                      seer, B, iters, flags, orig_player, max_depth, (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf,
-                     (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting, (uint64_t)0, (int32_t*)nullptr);
+                     (CfrState*)state, probs, feat, (CitOpt*)chosen, waiting, (uint64_t)0, (int32_t*)nullptr, d.base_off);
   CHECK_LAUNCH();
 }
 
@@ -394,10 +428,11 @@ int cit_cfr_pred_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np
       !mt_idx || !np_mt || !np_idx || !seer || !pool || !optbuf || !state || !probs || !feat || !chosen ||
       !waiting || (slice_ticks && !running))
     return -1;
-  hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), (size_t)cfr_dyn_lds_bytes(node_cap, edge_cap), stream,
+  DynLds d = dyn_lds(pool, node_cap, edge_cap);
+  hipLaunchKernelGGL(k_cfr_pred_step, dim3(B), dim3(64), d.bytes, stream,
                      (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer, B, iters, flags, orig_player, max_depth,
                      (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CfrState*)state, probs, feat,
-                     (CitOpt*)chosen, waiting, (uint64_t)slice_ticks, running);
+                     (CitOpt*)chosen, waiting, (uint64_t)slice_ticks, running, d.base_off);
   CHECK_LAUNCH();
 }
 

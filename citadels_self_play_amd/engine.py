@@ -77,7 +77,7 @@ PRED_GROUPS = int(os.environ.get("CIT_PRED_GROUPS", "3"))
 # round counts into its own slot, read once per batch), so a group's stream
 # never idles for the host's round turnaround; launches past the end find
 # every tree done and return at once
-PRED_AHEAD = int(os.environ.get("CIT_PRED_AHEAD", "1"))
+PRED_AHEAD = int(os.environ.get("CIT_PRED_AHEAD", "4"))
 PRED_SLICE_TICKS = int(os.environ.get("CIT_PRED_SLICE_TICKS", "0"))   # 1 / 2 / 3 / 4: 87.0k / 96.9k / 100.3k / 61.4k decisions/s (config 4, profiles/r03/pred_groups)
 _side_streams = {}
 

@@ -17,8 +17,9 @@ def build(name, extra):
     out = os.path.join(ROOT, "build", os.environ.get("ABDIR", "ab"))
     os.makedirs(out, exist_ok=True)
     o = os.path.join(out, name + ".o")
-    flags = [f for f in G.HIP_FLAGS if not (f.startswith("-O") and any(e.startswith("-O") for e in extra))]
     unit = os.environ.get("AB_UNIT", "cit_hip.hip")
+    flags = [f for f in G.HIP_FLAGS + G.UNIT_FLAGS.get(unit, [])
+             if not (f.startswith("-O") and any(e.startswith("-O") for e in extra))]
     subprocess.check_call([G.HIPCC] + flags + extra + ["-c", os.path.join(G.CSRC, unit), "-o", o])
     others = [os.path.join(ROOT, "build", "hip", u.replace(".hip", ".o")) for u in G.HIP_UNITS if u != unit]
     lib = os.path.join(out, "lib%s.so" % name)

@@ -44,17 +44,23 @@ Prints ONE JSON line on rank 0.  `value` = carry_out transitions of all ranks
   k_init) and rolled out, init + rollout of batch k on stream k % streams, so
   the next batch's seeding overlaps the previous batches' rollouts.
 * `cfr_configs` (default on; --no-cfr to skip) measures BASELINE configs 3-5,
-  the MCCFR workloads, each a dict with its own value / unit, the SURVEY
-  §8(d) CFR roofline (bytes per child created over the search time), and a
-  C++ CPU baseline (the same search headers built for the host,
-  cith_cfr_timed, 1 core and all usable cores):
+  the MCCFR workloads, each a dict with its own value / unit, a roofline and
+  a C++ CPU baseline (the same search headers built for the host,
+  cith_cfr_timed, 1 core and all usable cores).  The search kernels are
+  latency-bound (one wave per tree, a serial search), so `roofline` is the
+  issue / latency model from in-run counters (four rocprofv3 --pmc passes
+  over one `--pmc-child` run of the three workloads at small sizes, whose
+  kernels are distinct): SALU floor over the search time, wait fraction,
+  SALU / VALU / LDS / VMEM instructions and counter traffic per carry_out;
+  `hbm_notional` keeps SURVEY §8(d)'s bytes per child created:
     3: 1024 positions per GPU, one cfr_train(200) decision each (no NN)
     4: 4096 positions over the job (4096 / N per GPU), cfr_pred(200, depth 10)
        with ValueOnlyNN(418, 512) weights from torch.manual_seed(0)
     5: --cfg5-trees simulate_game trees per GPU at cfr_train(--cfg5-iters)
        (default 200000, the reference's own setting) through the tree queue,
        targets pooled with the RCCL all-gather
-  At N = 1, config 3 also carries in-run PMC passes of its search kernel.
+  `4@512` and `5@960` run configs 4 and 5 at the per-rank shard of the 8-GPU
+  job (4096 / 8 positions; train_from_scratch's --games-per-gpu trees).
   Config 3's `value` runs consecutive batches on --cfr-streams HIP streams
   (a continuous self-play loop, as config 2); `value_one_batch` is one batch
   at a time.
@@ -214,18 +220,24 @@ def _rows(pattern):
     return out
 
 
-def _pmc_pass(counters, outdir, config=2, timeout_s=150):
+def _pmc_pass(counters, outdir, config=2, timeout_s=150, cfr_child=False):
     """One rocprofv3 --pmc pass over a short child run of this script (its own
-    process group, killed on timeout).  Returns {counter: mean per launch of
-    the config's kernel} or raises."""
+    process group, killed on timeout).  Config 2: {counter: mean per launch of
+    k_rollout_u}.  cfr_child: the child runs configs 3 / 4 / 5 once each
+    (--pmc-child) and the result is {kernel: {counter: sum over its launches,
+    "_launches": n}, "_child": the child's JSON line}.  Raises on failure."""
     os.makedirs(outdir, exist_ok=True)
-    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(config), "--no-cpu-baseline", "--no-pmc",
-             "--no-cfr"]
-    child += ["--steps", "2", "--warmup", "1", "--streams", "1"] if config == 2 else [
-        "--cfr-reps", "1", "--cfg5-reps", "1", "--cfr-streams", "1"]
+    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-pmc"]
+    if cfr_child:
+        child += ["--pmc-child"]
+    else:
+        child += ["--config", str(config), "--no-cfr"]
+        child += ["--steps", "2", "--warmup", "1", "--streams", "1"] if config == 2 else [
+            "--cfr-reps", "1", "--cfg5-reps", "1", "--cfr-streams", "1"]
     cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", outdir, "-o", "run", "--"] + child
     env = dict(os.environ, TMPDIR="/tmp")
-    with open(os.path.join(outdir, "log.txt"), "w") as log:
+    logp = os.path.join(outdir, "log.txt")
+    with open(logp, "w") as log:
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
         try:
             rc = p.wait(timeout=timeout_s)
@@ -235,9 +247,27 @@ def _pmc_pass(counters, outdir, config=2, timeout_s=150):
             raise RuntimeError("rocprofv3 --pmc %s timed out" % counters)
     if rc != 0:
         raise RuntimeError("rocprofv3 --pmc %s exited %d" % (counters, rc))
+    rows = _rows(os.path.join(outdir, "**", "*counter_collection.csv"))
+    if cfr_child:
+        out = {}
+        for kernel in (KERNELS[3], KERNELS[4], KERNELS[5]):
+            per = {}
+            for r in rows:
+                if kernel in r.get("Kernel_Name", ""):
+                    per.setdefault(r["Counter_Name"], {}).setdefault(r.get("Dispatch_Id", "0"), 0.0)
+                    per[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
+            if per:
+                out[kernel] = {k: sum(v.values()) for k, v in per.items()}
+                out[kernel]["_launches"] = max(len(v) for v in per.values())
+        with open(logp) as f:
+            lines = [ln for ln in f if ln.startswith("{\"pmc_child\"")]
+        if not out or not lines:
+            raise RuntimeError("no search-kernel rows / child line in the rocprofv3 output")
+        out["_child"] = json.loads(lines[-1])
+        return out
     kernel = KERNELS[config]
     per = {}
-    for r in _rows(os.path.join(outdir, "**", "*counter_collection.csv")):
+    for r in rows:
         if kernel in r.get("Kernel_Name", ""):
             per.setdefault(r["Counter_Name"], {}).setdefault(r.get("Dispatch_Id", "0"), 0.0)
             per[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
@@ -262,6 +292,66 @@ def pmc_in_run(config=2):
         out["sq"] = _pmc_pass(SQ_SET, os.path.join(base, "sq"), config)
     except Exception as e:  # a missing profiler must not cost the bench line
         out["error"] = str(e)[:300]
+    return out
+
+
+# Counter passes over one --pmc-child run of the three search workloads (their
+# kernels are distinct, so one child serves configs 3, 4 and 5).
+CFR_PMC_PASSES = (["FETCH_SIZE"], ["WRITE_SIZE"], SQ_SET, ["SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"])
+PMC_CHILD = {3: 1024, 4: 4096, 5: 128}          # positions / trees per config in the --pmc-child run
+
+
+def pmc_in_run_cfr():
+    """Four --pmc passes over `bench.py --pmc-child` (configs 3, 4, 5 once each
+    at PMC_CHILD sizes, no warm-up).  Returns {config: {counter: total,
+    "carry_outs": the child's carry_outs, "search_ms": its search time}}."""
+    base = tempfile.mkdtemp(prefix="bench_pmc_cfr_", dir="/tmp")
+    out = {}
+    try:
+        for i, ctrs in enumerate(CFR_PMC_PASSES):
+            r = _pmc_pass(ctrs, os.path.join(base, "p%d" % i), cfr_child=True, timeout_s=240)
+            child = r.pop("_child")
+            for c in (3, 4, 5):
+                k = KERNELS[c]
+                d = out.setdefault(c, {"kernel": k, "source": "in-run rocprofv3 --pmc, %d passes over one "
+                                       "`bench.py --pmc-child` run (%d %s)" % (len(CFR_PMC_PASSES), PMC_CHILD[c],
+                                                                         "trees" if c == 5 else "positions")})
+                d.update(r.get(k, {}))
+                d["carry_outs_pass%d" % i] = child[str(c)]["carry_outs"]
+                d["search_ms_pass%d" % i] = child[str(c)]["search_ms"]
+                d["carry_outs"] = child[str(c)]["carry_outs"]
+    except Exception as e:  # a missing profiler must not cost the bench line
+        out["error"] = str(e)[:300]
+    return out
+
+
+def search_roofline(pmc, alg_bytes_per_carry):
+    """The latency / issue model of a search kernel from its in-run counters
+    (totals over the child's launches, priced per carry_out): SALU floor over
+    the child's search time, wait fraction, VMEM instructions and counter
+    traffic per carry_out against SURVEY §8(d)'s algorithmic bytes."""
+    if not pmc or "SQ_INSTS_SALU" not in pmc:
+        return None
+    carry = float(pmc["carry_outs"])
+    ms = float(pmc.get("search_ms_pass2") or 0.0)            # the SQ pass's own search time
+    salu = pmc["SQ_INSTS_SALU"]
+    salu_floor_ms = salu / SALU_PEAK * 1e3
+    out = {"salu_per_carry_out": salu / carry, "valu_per_carry_out": pmc.get("SQ_INSTS_VALU", 0.0) / carry,
+           "lds_per_carry_out": pmc.get("SQ_INSTS_LDS", 0.0) / carry,
+           "smem_per_carry_out": pmc.get("SQ_INSTS_SMEM", 0.0) / carry,
+           "salu_floor_ms": salu_floor_ms, "search_ms": ms, "salu_frac": salu_floor_ms / ms if ms else None,
+           "salu_inst_per_s": salu / (ms * 1e-3) if ms else None, "launches": pmc.get("_launches")}
+    if pmc.get("SQ_WAVE_CYCLES"):
+        out["wait_any_frac"] = pmc.get("SQ_WAIT_ANY", 0.0) / pmc["SQ_WAVE_CYCLES"]
+    if "SQ_INSTS_VMEM_RD" in pmc:
+        c3 = float(pmc.get("carry_outs_pass3", carry))
+        out["vmem_rd_per_carry_out"] = pmc["SQ_INSTS_VMEM_RD"] / c3
+        out["vmem_wr_per_carry_out"] = pmc.get("SQ_INSTS_VMEM_WR", 0.0) / c3
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        c0, c1 = float(pmc.get("carry_outs_pass0", carry)), float(pmc.get("carry_outs_pass1", carry))
+        per = 2 * 1024 * pmc["FETCH_SIZE"] / c0 + 1024 * pmc["WRITE_SIZE"] / c1
+        out["traffic_bytes_per_carry_out"] = per
+        out["traffic_over_alg"] = per / alg_bytes_per_carry if alg_bytes_per_carry else None
     return out
 
 
@@ -516,22 +606,26 @@ def _value_net(dev):
     return models.ValueNet(m, dev)
 
 
-def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
+def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, warm_rep=True, n_reps=None):
     """One of BASELINE configs 3-5 (tools/bench_selfplay.py's harness): median
-    of `args.cfr_reps` timed reps after one warm-up.  Returns a dict (rank 0)."""
+    of `args.cfr_reps` timed reps after one warm-up.  `per_gpu` overrides the
+    positions / trees per GPU (the per-rank shard of an 8-GPU config).  `pmc`:
+    this config's entry of pmc_in_run_cfr.  Returns a dict (rank 0)."""
     from citadels_self_play_amd import layout as L
     from citadels_self_play_amd import selfplay
     from citadels_self_play_amd.engine import GameBatch, pool_caps
     iters = {3: 200, 4: 200, 5: args.cfg5_iters}[config]
-    per_gpu = {3: 1024, 4: max(1, 4096 // world), 5: args.cfg5_trees}[config]
+    if per_gpu is None:
+        per_gpu = {3: 1024, 4: max(1, 4096 // world), 5: args.cfg5_trees}[config]
     net = _value_net(dev) if config == 4 else None
     # one 4096-node block per tree either way; room enough that no config-3/4 tree
     # overflows into the (serial) retry
     node_cap = {3: 4096, 4: 4096}.get(config)
     reps = []
     stream = torch.cuda.current_stream()
-    n_reps = args.cfg5_reps if config == 5 else args.cfr_reps
-    for rep in range(1 + n_reps):
+    if n_reps is None:
+        n_reps = args.cfg5_reps if config == 5 else args.cfr_reps
+    for rep in range(0 if warm_rep else 1, 1 + n_reps):
         warm = rep == 0
         n = per_gpu if not (warm and config == 5) else min(per_gpu, 64)
         it = iters if not (warm and config == 5) else min(iters, 2000)
@@ -566,11 +660,14 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
             continue
         st = stats.to(dev).to(torch.float64)
         bad = ((st[:, 4] != 0) & ~term.to(dev)).sum()
-        el_max, units, carry, nodes, edges, errs, terms = _reduce(
-            [el, st.shape[0], st[:, 3].sum(), st[:, 1].sum(), st[:, 2].sum(), bad, term.sum()], world, dev, maxes=(0,))
+        _, cls = selfplay.error_classes(stats, term)
+        el_max, units, carry, nodes, edges, errs, terms, *ncls = _reduce(
+            [el, st.shape[0], st[:, 3].sum(), st[:, 1].sum(), st[:, 2].sum(), bad, term.sum()] +
+            [cls[k] for k in selfplay.ERROR_CLASSES], world, dev, maxes=(0,))
         reps.append({"seconds": el_max, "gpu_ms_rank0": ev[0].elapsed_time(ev[1]), "units": units,
                      "value": units / el_max, "carry_out_per_s": carry / el_max, "nodes": nodes, "edges": edges,
                      "error_lanes_nonterminal": int(errs), "terminal_positions": int(terms), "leaf_rounds": rounds,
+                     "error_classes": {k: int(v) for k, v in zip(selfplay.ERROR_CLASSES, ncls)},
                      "pooled_targets": n_targets})
     streams = None
     if config == 3 and args.cfr_streams > 1:
@@ -583,33 +680,39 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True):
     alg = med["nodes"] * 5 * S + 24.0 * med["edges"]
     ms = med["seconds"] * 1e3
     achieved = alg / world / med["seconds"] / 1e9          # per GPU
+    carry_all = med["carry_out_per_s"] * med["seconds"]
+    hbm_notional = {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                    "alg_bytes": alg, "alg_bytes_per_carry_out": alg / max(1.0, carry_all), "search_ms": ms,
+                    "model": "SURVEY §8(d) CFR expand bytes: 5 x CIT_GAME_BYTES per node created + 24 B per edge "
+                             "slot, over the search's wall time per GPU"}
+    issue = search_roofline(pmc, alg / max(1.0, carry_all)) if pmc else None
+    if issue is not None and issue.get("salu_frac") is not None:
+        roof = {"bound": "latency (salu-issue floor)", "achieved": issue["salu_inst_per_s"] / 1e9,
+                "peak": SALU_PEAK / 1e9, "unit": "G SALU inst/s", "frac": issue["salu_frac"],
+                "traffic_bytes_per_carry_out": issue.get("traffic_bytes_per_carry_out"),
+                "traffic": issue.get("traffic_bytes_per_carry_out"),
+                "model": "one wave per tree runs a serial search: the SALU floor (SQ_INSTS_SALU / (256 CU x 2.4 "
+                         "GHz)) over the search time of the counter run, with its wait fraction and VMEM "
+                         "instructions per carry_out; hbm_notional keeps SURVEY §8(d)'s bytes"}
+    else:
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "note": "no SQ counters for this leg: SURVEY §8(d)'s notional HBM figure"}
+    roof.update({"kernel": KERNELS[config], "issue": issue, "hbm_notional": hbm_notional, "pmc": pmc,
+                 "search_ms": ms})
     out = {"config": config, "workload": {
         3: "config3: %d positions per GPU (preset game + U[0,300] random steps), one cfr_train(200) decision each"
            % per_gpu,
-        4: "config4: %d positions per GPU (4096 over the job), cfr_pred(200, depth 10) + ValueOnlyNN(418,512) "
-           "leaves (torch.manual_seed(0) weights)" % per_gpu,
+        4: "config4: %d positions per GPU (%d over the job), cfr_pred(200, depth 10) + ValueOnlyNN(418,512) "
+           "leaves (torch.manual_seed(0) weights)" % (per_gpu, per_gpu * world),
         5: "config5: %d simulate_game trees per GPU: create_a_random_game(100) -> cfr_train(%d) -> "
            "get_all_targets(200), tree queue, targets all-gathered" % (per_gpu, iters)}[config],
+        "per_gpu": per_gpu,
         "value": streams["value"] if streams else med["value"], "unit": "trees/s" if config == 5 else "decisions/s",
         "value_one_batch": med["value"], "streams": streams,
         "carry_out_per_s": med["carry_out_per_s"], "reps": len(reps), "median": med,
         "all_reps_value": [r["value"] for r in reps],
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "kernel": KERNELS[config],
-                     "alg_bytes": alg, "search_ms": ms,
-                     "model": "SURVEY §8(d) CFR expand bytes: 5 x CIT_GAME_BYTES per node created + 24 B per edge "
-                              "slot, over the search's wall time per GPU (the search is a serial latency chain per "
-                              "tree: see issue / DESIGN.md §5)"}}
-    if pmc:
-        sq = pmc.get("sq")
-        launches = (sq or {}).get("_launches", 1)
-        if sq and config == 3:
-            # the child runs one config-3 batch per launch: price per carry_out of that batch
-            carry_per_launch = med["carry_out_per_s"] * med["seconds"] / max(1, world)
-            out["roofline"]["issue"] = issue_roofline(sq, carry_per_launch, med["gpu_ms_rank0"], unit="carry_out")
-        out["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch")
-        out["roofline"]["pmc"] = pmc
-        out["roofline"]["pmc_launches"] = launches
+        "roofline": roof}
     if cpu and world == 1 and not args.no_cpu_baseline:
         w = None
         if config == 4:
@@ -688,7 +791,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 --pmc passes")
     ap.add_argument("--no-cfr", action="store_true", help="skip the configs 3-5 legs (cfr_configs)")
-    ap.add_argument("--cfr-configs", default="3,4,5")
+    ap.add_argument("--cfr-configs", default="3,4,5,4@512,5@960",
+                    help="configs 3-5; C@N runs config C at N positions / trees per GPU (4@512: the per-rank shard of "
+                         "config 4's 4096 positions over 8 GPUs; 5@960: train_from_scratch's --games-per-gpu)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cfr-reps", type=int, default=5, help="timed reps of configs 3 and 4 (median reported)")
     ap.add_argument("--cfg5-reps", type=int, default=1, help="timed reps of config 5")
     ap.add_argument("--cfr-cpu-seconds", type=float, default=4.0, help="per C++ CPU-baseline leg of configs 3-5")
@@ -710,11 +816,23 @@ def main():
     if folded and args.dist_backend == "nccl":
         raise SystemExit("bench.py: WORLD_SIZE=%d > %d visible GPUs; RCCL needs one rank per GPU "
                          "(use --dist-backend gloo to rehearse folded ranks)" % (world, n_dev))
-    cfr_list = [] if args.no_cfr or args.config != 2 else [int(c) for c in args.cfr_configs.split(",") if c.strip()]
+    cfr_list = [] if args.no_cfr or args.config != 2 else [c.strip() for c in args.cfr_configs.split(",") if c.strip()]
+
+    if args.pmc_child:          # the counter runs of pmc_in_run_cfr: configs 3, 4, 5 once each, small
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        args.cfr_streams = 1
+        line = {"pmc_child": 1}
+        for c in (3, 4, 5):
+            r = run_cfr(c, args, 1, 0, dev, cpu=False, per_gpu=PMC_CHILD[c], warm_rep=False, n_reps=1)
+            m = r["median"]
+            line[str(c)] = {"carry_outs": m["carry_out_per_s"] * m["seconds"], "search_ms": m["seconds"] * 1e3}
+        print(json.dumps(line), flush=True)
+        return
 
     # The PMC passes run as child processes before this process touches the GPU.
-    pmc = pmc_in_run(args.config) if (world == 1 and not args.no_pmc) else None
-    cfr_pmc = pmc_in_run(3) if (world == 1 and not args.no_pmc and 3 in cfr_list) else None
+    pmc = pmc_in_run(2) if (args.config == 2 and world == 1 and not args.no_pmc) else None
+    cfr_pmc = pmc_in_run_cfr() if (world == 1 and not args.no_pmc and (cfr_list or args.config != 2)) else {}
 
     dev = torch.device("cuda", local % max(1, n_dev))
     if world > 1:
@@ -725,7 +843,7 @@ def main():
     if args.config == 2:
         out = run_rollout(args, world, rank, dev, n_dev, pmc)
     else:
-        c = run_cfr(args.config, args, world, rank, dev, pmc=pmc)
+        c = run_cfr(args.config, args, world, rank, dev, pmc=cfr_pmc.get(args.config))
         out = None
         if rank == 0:
             out = {"metric": "MCCFR config %d" % args.config, "value": c["value"], "unit": c["unit"],
@@ -735,11 +853,20 @@ def main():
                    "config": {"workload": c["workload"], "parallelism": "dp%d" % world},
                    "roofline": c["roofline"], "cpu_baseline": c.get("cpu_baseline"), "cfr": c}
     cfr_out = {}
-    for c in cfr_list:
+    for key in cfr_list:
         try:
-            cfr_out[str(c)] = run_cfr(c, args, world, rank, dev, pmc=cfr_pmc if c == 3 else None)
+            c, _, n = key.partition("@")
+            c = int(c)
+            r = run_cfr(c, args, world, rank, dev, pmc=None if n else cfr_pmc.get(c), per_gpu=int(n) if n else None,
+                        cpu=not n)
+            if n and r is not None:
+                r["shard_of"] = {4: "config 4's 4096 positions over 8 GPUs (the per-rank work of that config)",
+                                 5: "config 5 / train_from_scratch at its default --games-per-gpu"}.get(c)
+            cfr_out[key] = r
         except Exception as e:          # a CFR leg must not cost the headline line
-            cfr_out[str(c)] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
+            cfr_out[key] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
+    if cfr_pmc.get("error") and rank == 0:
+        cfr_out["pmc_error"] = cfr_pmc["error"]
 
     if rank == 0:
         if folded:

@@ -27,8 +27,10 @@
 #define CFR_OPP_CHILDREN 10
 #define CFR_ROLE_CHILDREN 10
 #define CFR_OPT_CAP 512
+// options listed into LDS per search step
 #ifndef CFR_LBUF
 #define CFR_LBUF 32
+#endif
 // update_strategy's LDS copies of S / CS (CfrLds.sbuf / cbuf) hold the nodes
 // with up to CFR_SBUF children (at most 55 seen in 64 cfr_train(2000) trees);
 // a node with more runs the host build's loop over its edge records in HBM
@@ -37,8 +39,6 @@
 #ifndef CFR_SBUF
 #define CFR_SBUF 96
 #endif
-#endif
-// options listed into LDS per search step
 #define CFR_LN13 0x1.0ca937be1b9dcp-2   // np.log(1.3)
 #define CFR_ATOL 1.4901161193847656e-08  // sqrt(finfo(float64).eps), numpy choice's p check
 
@@ -89,7 +89,8 @@ static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
 // CFR_ROW_HDR words (bit d of the 388-bit mask in words 0..12 = dword d differs
 // from the base; word 13 the count) and then the differing dwords in index
 // order, at most K.  A cfr_train(200000) node differs from its root in ~70 of
-// 388 dwords (max ~100 measured), so K = 128 halves a node's bytes; a row
+// 388 dwords (max ~100 measured), so K = 128 cuts a node's record + row slot
+// from 1,720 to 744 B (0.43x; with its ~4 edge slots 1.9 KB -> 0.94 KB); a row
 // with more than K differing dwords stops the tree with CIT_ERR_OVERFLOW and
 // the tree is searched again with raw rows (engine.py's retry): the slot size
 // never changes a result.
@@ -711,7 +712,7 @@ CIT_HD CitOpt opt_key(const CitOpt& o, const CitGame& g) {
       break;
     case O_DISCARD_AND_DRAW:
     case O_CARDINAL:
-      for (int i = 0; i < P.n_hand; i++)
+      for (int i = 0; i < P.n_hand && i < CIT_HAND_MASK_MAX; i++)
         if ((o.x >> i) & 1) h = type_seq_hash(h, card_type(P.hand[i]));
       k.x = h;
       break;

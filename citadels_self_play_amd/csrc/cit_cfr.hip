@@ -41,8 +41,11 @@ __device__ __forceinline__ void mt_stage_out(const uint32_t* src, uint32_t* mt, 
 }
 
 // The tree's LDS block (cit_cfr.h, cfr_ls): pool binding (block tables in LDS),
-// streams, working rows.
-__device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx,
+// streams, working rows.  False when the pool stores diff rows but the launch
+// reserved no dynamic LDS for the base row (base_off < 0: the library's record
+// of the pool's row format disagrees with the arena header); the kernel then
+// stops the tree with CIT_ERR_UNSUPPORTED instead of addressing cfr_dyn[-1].
+__device__ __forceinline__ bool tree_setup(uint32_t* mt, uint32_t* idx, uint32_t* npmt, uint32_t* npidx,
                                            uint64_t* seer, int B, long l, uint8_t* pool, int node_cap, int edge_cap,
                                            CitOpt* optbuf, int flags, int base_off) {
   CfrTree& T = cfr_ls.T;
@@ -62,6 +65,7 @@ __device__ __forceinline__ void tree_setup(uint32_t* mt, uint32_t* idx, uint32_t
   T.w1 = reinterpret_cast<CitGame*>(cfr_ls.w[1]);
   T.tmp = cfr_ls.tmp;
   T.lbuf = cfr_ls.lbuf;
+  return !(T.row_cap != 0 && base_off < 0);
 }
 
 // The block tables (and, for diff row slots, the base row) of a resumed tree
@@ -109,7 +113,15 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_decide(uint32_t* games, uint
 #endif
   cfr_prof_reset();
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off);
+  if (!tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off)) {
+    if (threadIdx.x == 0) {
+      chosen[l] = mk(O_NUM_NAMES, 0);
+      stats[5 * l + 0] = -1;
+      stats[5 * l + 1] = stats[5 * l + 2] = stats[5 * l + 3] = 0;
+      stats[5 * l + 4] = (int)CIT_ERR_UNSUPPORTED;
+    }
+    return;
+  }
   T.n_nodes = T.n_edges = 0;
   T.err = 0;
   T.carry_outs = 0;
@@ -160,7 +172,16 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_pred_step(uint32_t* games, u
   S = state[l];             // every lane stores the same value
   if (S.phase == CP_DONE) return;
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off);
+  if (!tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off)) {
+    if (threadIdx.x == 0) {
+      S.err |= (int)CIT_ERR_UNSUPPORTED;
+      S.root = -1;
+      S.phase = CP_DONE;
+      state[l] = S;
+      chosen[l] = mk(O_NUM_NAMES, 0);
+    }
+    return;
+  }
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;
@@ -210,7 +231,19 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_train_slice(uint32_t* games,
   S = state[l];
   if (S.phase == CP_DONE) return;
   CfrTree& T = cfr_ls.T;
-  tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off);
+  if (!tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off)) {
+    if (threadIdx.x == 0) {
+      S.err |= (int)CIT_ERR_UNSUPPORTED;
+      S.root = -1;
+      S.phase = CP_DONE;
+      state[l] = S;
+      chosen[l] = mk(O_NUM_NAMES, 0);
+      stats[5 * l + 0] = -1;
+      stats[5 * l + 1] = stats[5 * l + 2] = stats[5 * l + 3] = 0;
+      stats[5 * l + 4] = (int)CIT_ERR_UNSUPPORTED;
+    }
+    return;
+  }
   if (S.phase == CP_INIT) {
     T.n_nodes = T.n_edges = 0;
     T.err = 0;

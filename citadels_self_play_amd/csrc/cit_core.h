@@ -49,17 +49,28 @@ __device__ __forceinline__ uint64_t cit_wave_or64(uint64_t v) {
 #endif
 
 // ---------------------------------------------------------------- capacities
+// A player's hand, just-drawn cards and museum share one card area of
+// CIT_AREA_CAP slots (CitPlayer::hand, back to back in that order): the
+// reference's lists have no caps, and one player can only hold more than 88
+// cards if the game has more cards than the 76 it deals (66 in random-role
+// games) -- a reference game gains cards only through get_a_card_like_it's
+// fallback (deck.py:49-55), one at a time.  Buildings stay a list of their own
+// (the rules end the game a round after 7).  (#ifndef: tools/capstats.cpp
+// builds the host engine with wider lists to measure how long they get.)
 #define CIT_NP 6
-#define CIT_HAND_CAP 32
+#ifndef CIT_AREA_CAP
+#define CIT_AREA_CAP 88
+#endif
+#ifndef CIT_BUILD_CAP
 #define CIT_BUILD_CAP 16
-#define CIT_JD_CAP 40
-#define CIT_MUSEUM_CAP 16
+#endif
 #define CIT_DECK_CAP 128          // ring buffer, power of two
-#define CIT_DISCARD_CAP 80
+#define CIT_DISCARD_CAP 88        // >= the 76 cards a game deals
 #define CIT_USED_CAP 80
 #define CIT_KH_MAX 32
-#define CIT_KH_POOL 252
+#define CIT_KH_POOL 244          // cards held by HandKnowledge entries (88 at most in 1,920 cfr_train(200000) trees)
 #define CIT_SEVEN_CAP 8
+#define CIT_HAND_MASK_MAX 60      // magician / cardinal hand-slot masks (uint64_t) and binom() range
 
 // ------------------------------------------------------------------- errors
 // A lane whose reference run would raise (or that overflows a fixed capacity)
@@ -140,10 +151,9 @@ struct CitOpt {
 
 // ------------------------------------------------------------- packed game
 struct CitPlayer {                 // 128 B
-  uint8_t hand[CIT_HAND_CAP];
+  uint8_t hand[CIT_AREA_CAP];      // card area: hand [0, n_hand) | just_drawn_cards
+                                   // [n_hand, +n_jd) | museum_cards [.., +n_museum)
   uint8_t build[CIT_BUILD_CAP];
-  uint8_t jd[CIT_JD_CAP];          // just_drawn_cards
-  uint8_t museum[CIT_MUSEUM_CAP];
   uint8_t n_hand, n_build, n_jd, n_museum;
   int16_t gold;
   uint8_t role;                    // role index / ROLE_BEWITCHED / ROLE_NONE
@@ -164,7 +174,7 @@ struct CitKH {                     // one HandKnowledge entry, 4 B
 };
 
 struct CitGame {
-  CitPlayer pl[CIT_NP];            // 672
+  CitPlayer pl[CIT_NP];            // 768
   uint8_t deck[CIT_DECK_CAP];      // ring: logical i at (deck_head+i) & (CAP-1)
   uint8_t discard[CIT_DISCARD_CAP];
   uint8_t used_cards[CIT_USED_CAP];
@@ -206,8 +216,11 @@ struct CitGame {
 enum { RP_DEAD = 1, RP_WARRANT_SHIFT = 1, RP_POSSESSED = 8, RP_ROBBED = 16, RP_BLACKMAIL_SHIFT = 5 };
 enum { WB_NONE = 0, WB_REAL = 1, WB_FAKE = 2 };
 
+#ifndef CIT_GAME_BYTES
 #define CIT_GAME_BYTES 1552
+#endif
 static_assert(sizeof(CitGame) <= CIT_GAME_BYTES, "CitGame grew past its row size");
+static_assert(CIT_AREA_CAP <= 128, "card area: at most two bytes per lane");
 static_assert(CIT_GAME_BYTES % 16 == 0, "row must be 16-byte aligned");
 
 // Optional per-function cycle accounting (build with -DCIT_PROF; profiling

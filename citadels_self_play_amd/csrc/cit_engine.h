@@ -74,9 +74,18 @@ CIT_HD int take_like(uint8_t* a, uint8_t& n, int c) {
   }
   return c;
 }
+// Length statistics (host measurement builds only, tools/capstats.cpp): the
+// tool defines cit_cap_note and sees every append's resulting length.
+#if defined(CIT_CAP_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+void cit_cap_note(const CitGame& g, const void* list, int n);
+#define CIT_CAP_NOTE(g, a, n) cit_cap_note(g, a, n)
+#else
+#define CIT_CAP_NOTE(g, a, n) ((void)0)
+#endif
 // Deck.add_card (deck.py:62-67): the "Deck Empty" sentinel (CIT_NO_CARD) is dropped.
 CIT_HD void put_card(CitGame& g, uint8_t* a, uint8_t& n, int cap, int c) {
   if (c == CIT_NO_CARD) return;
+  CIT_CAP_NOTE(g, a, n + 1);
   if (n >= cap) { g.err |= CIT_ERR_OVERFLOW; return; }
   a[n++] = (uint8_t)c;
 }
@@ -112,10 +121,111 @@ struct ByteList {
 #endif
 };
 
-#define HAND(p) (p).hand, (p).n_hand, CIT_HAND_CAP
 #define BUILD(p) (p).build, (p).n_build, CIT_BUILD_CAP
-#define JD(p) (p).jd, (p).n_jd, CIT_JD_CAP
-#define MUSEUM(p) (p).museum, (p).n_museum, CIT_MUSEUM_CAP
+
+// ------------------------------------------------- a player's card area
+// hand | just_drawn_cards | museum_cards back to back in CitPlayer::hand
+// (cit_core.h).  A list starts where the lists before it end; every change of
+// a list's length goes through the functions below, which move the lists
+// after it.  Reads index the area directly (the hand at 0, pl_jd, pl_museum).
+enum { AL_HAND = 0, AL_JD = 1, AL_MUSEUM = 2 };
+CIT_HD int area_used(const CitPlayer& P) { return P.n_hand + P.n_jd + P.n_museum; }
+CIT_HD int area_off(const CitPlayer& P, int L) { return L == AL_HAND ? 0 : L == AL_JD ? P.n_hand : P.n_hand + P.n_jd; }
+CIT_HD int area_len(const CitPlayer& P, int L) { return L == AL_HAND ? P.n_hand : L == AL_JD ? P.n_jd : P.n_museum; }
+CIT_HD void area_set_len(CitPlayer& P, int L, int n) {
+  (L == AL_HAND ? P.n_hand : L == AL_JD ? P.n_jd : P.n_museum) = (uint8_t)n;
+}
+CIT_HD const uint8_t* pl_jd(const CitPlayer& P) { return P.hand + P.n_hand; }
+CIT_HD const uint8_t* pl_museum(const CitPlayer& P) { return P.hand + P.n_hand + P.n_jd; }
+#if defined(CIT_CAP_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+void cit_area_note(const CitGame& g, const CitPlayer& P);
+#define CIT_AREA_NOTE(g, P) cit_area_note(g, P)
+#else
+#define CIT_AREA_NOTE(g, P) ((void)0)
+#endif
+
+// List L of P: its elements [at, at + del) are replaced by src(0), ..,
+// src(ins - 1) (the reference's list surgery: append, remove, pop(0), clear,
+// reassign); the lists after L move by ins - del.  An area past CIT_AREA_CAP
+// sets the overflow bit and changes nothing.  Wave: lane l moves the area
+// bytes at l and l + 64 past the cut and writes src(l) and src(l + 64); every
+// load precedes every store, so src may read the area.
+template <class Src>
+CIT_HD void area_splice(CitGame& g, CitPlayer& P, int L, int at, int del, int ins, Src src) {
+  const int used = area_used(P), cut = area_off(P, L) + at;
+  if (used - del + ins > CIT_AREA_CAP) { g.err |= CIT_ERR_OVERFLOW; return; }
+#if CIT_WAVE
+  {
+    const int l = cit_lane(), j0 = cut + del + l, j1 = j0 + 64;
+    const int v0 = j0 < used ? P.hand[j0] : 0, v1 = j1 < used ? P.hand[j1] : 0;
+    const int s0 = l < ins ? (int)src(l) : 0, s1 = l + 64 < ins ? (int)src(l + 64) : 0;
+    __asm__ volatile("" ::: "memory");   // every byte loaded before any is stored
+    if (j0 < used) P.hand[j0 - del + ins] = (uint8_t)v0;
+    if (j1 < used) P.hand[j1 - del + ins] = (uint8_t)v1;
+    if (l < ins) P.hand[cut + l] = (uint8_t)s0;
+    if (l + 64 < ins) P.hand[cut + l + 64] = (uint8_t)s1;
+  }
+#else
+  {
+    uint8_t tmp[CIT_AREA_CAP];
+    for (int i = 0; i < ins; i++) tmp[i] = (uint8_t)src(i);
+    const int shift = ins - del, from = cut + del, tail = used - from;
+    if (shift > 0)
+      for (int i = tail - 1; i >= 0; i--) P.hand[from + i + shift] = P.hand[from + i];
+    else if (shift < 0)
+      for (int i = 0; i < tail; i++) P.hand[from + i + shift] = P.hand[from + i];
+    for (int i = 0; i < ins; i++) P.hand[cut + i] = tmp[i];
+  }
+#endif
+  area_set_len(P, L, area_len(P, L) - del + ins);
+  CIT_AREA_NOTE(g, P);
+}
+// Deck.add_card on list L (the "Deck Empty" sentinel, CIT_NO_CARD, is dropped)
+CIT_HD void pl_put(CitGame& g, CitPlayer& P, int L, int c) {
+  if (c == CIT_NO_CARD) return;
+  area_splice(g, P, L, area_len(P, L), 0, 1, [c](int) { return c; });
+}
+// Deck.get_a_card_like_it on list L: removes the first card of c's type and
+// returns it, or returns c itself when there is none.  Wave: one load of the
+// list and the lists after it, one ballot, one store of the moved bytes.
+CIT_HD int pl_take_like(CitGame& g, CitPlayer& P, int L, int c) {
+  const int t = card_type(c), off = area_off(P, L), n = area_len(P, L);
+#if CIT_WAVE
+  {
+    const int used = area_used(P), l = cit_lane(), p0 = off + l, p1 = p0 + 64;
+    const int v0 = p0 < used ? P.hand[p0] : 0, v1 = p1 < used ? P.hand[p1] : 0;
+    const uint64_t m0 = cit_ballot(l < n && card_type(v0) == t), m1 = cit_ballot(l + 64 < n && card_type(v1) == t);
+    if (!(m0 | m1)) return c;
+    const int i = m0 ? __ffsll((unsigned long long)m0) - 1 : 64 + __ffsll((unsigned long long)m1) - 1;
+    const int r = i < 64 ? cit_readlane(v0, i) : cit_readlane(v1, i - 64);
+    if (l > i && p0 < used) P.hand[p0 - 1] = (uint8_t)v0;
+    if (l + 64 > i && p1 < used) P.hand[p1 - 1] = (uint8_t)v1;
+    area_set_len(P, L, n - 1);
+    return r;
+  }
+#endif
+  for (int i = 0; i < n; i++) {
+    int r = P.hand[off + i];
+    if (card_type(r) == t) {
+      area_splice(g, P, L, i, 1, 0, [](int) { return 0; });
+      return r;
+    }
+  }
+  return c;
+}
+// list L emptied (`.cards = []`)
+CIT_HD void pl_clear(CitGame& g, CitPlayer& P, int L) {
+  const int n = area_len(P, L);
+  if (area_off(P, L) + n == area_used(P)) area_set_len(P, L, 0);   // nothing after it moves
+  else area_splice(g, P, L, 0, n, 0, [](int) { return 0; });
+}
+// Deck.draw_card (pop(0)) on list L; CIT_NO_CARD when empty
+CIT_HD int pl_pop_front(CitGame& g, CitPlayer& P, int L) {
+  if (!area_len(P, L)) return CIT_NO_CARD;
+  const int r = P.hand[area_off(P, L)];
+  area_splice(g, P, L, 0, 1, 0, [](int) { return 0; });
+  return r;
+}
 CIT_HD bool p_has(const CitPlayer& p, int t) { return has_type(p.build, p.n_build, t); }
 // bit t set iff a card of type t is in the list
 CIT_HD uint64_t type_mask(const uint8_t* a, int n) {
@@ -164,6 +274,7 @@ CIT_HD int deck_draw(CitGame& g) {
 }
 CIT_HD void deck_put(CitGame& g, int c) {
   if (c == CIT_NO_CARD) return;
+  CIT_CAP_NOTE(g, g.deck, g.n_deck + 1);
   if (g.n_deck >= CIT_DECK_CAP - 1) { g.err |= CIT_ERR_OVERFLOW; return; }
   deck_ref(g, g.n_deck) = (uint8_t)c;
   g.n_deck++;
@@ -238,17 +349,15 @@ CIT_HD void reshuffle_if_empty(CitGame& g, CitMT& rng) {
   g.n_deck = g.n_discard;
   g.n_discard = 0;
 }
-CIT_HD void draw_into(CitGame& g, CitMT& rng, uint8_t* a, uint8_t& n, int cap, int k) {
+// k draws from the deck onto list L of P (each reshuffling the discard pile
+// into an empty deck first); wave: when the deck holds k cards and the area has
+// room, the k front cards move in one splice.
+CIT_HD void pl_draw(CitGame& g, CitMT& rng, CitPlayer& P, int L, int k) {
 #if CIT_WAVE
   {
-    // enough cards in the deck (no reshuffle) and room in the list: the k
-    // front cards move in one load + one store by k lanes
-    int nd = g.n_deck, head = g.deck_head, na = n;
-    if (k <= 64 && nd >= k && na + k <= cap) {
-      int l = cit_lane();
-      int c = g.deck[(head + l) & (CIT_DECK_CAP - 1)];
-      if (l < k) a[na + l] = (uint8_t)c;
-      n = (uint8_t)(na + k);
+    const int nd = g.n_deck, head = g.deck_head;
+    if (k <= 64 && nd >= k && area_used(P) + k <= CIT_AREA_CAP) {
+      area_splice(g, P, L, area_len(P, L), 0, k, [&g, head](int i) { return g.deck[(head + i) & (CIT_DECK_CAP - 1)]; });
       g.deck_head = (uint8_t)((head + k) & (CIT_DECK_CAP - 1));
       g.n_deck = (uint8_t)(nd - k);
       return;
@@ -257,7 +366,7 @@ CIT_HD void draw_into(CitGame& g, CitMT& rng, uint8_t* a, uint8_t& n, int cap, i
 #endif
   for (int i = 0; i < k; i++) {
     reshuffle_if_empty(g, rng);
-    put_card(g, a, n, cap, deck_draw(g));
+    pl_put(g, P, L, deck_draw(g));
   }
 }
 
@@ -270,6 +379,8 @@ CIT_HD int kh_off(const CitGame& g, int e) {
 }
 template <class At>
 CIT_HD void kh_append(CitGame& g, int owner, int target, int conf, bool wizard, int n, At card_at) {
+  CIT_CAP_NOTE(g, g.kh, g.n_kh + 1);
+  CIT_CAP_NOTE(g, g.kh_pool, g.kh_fill + n);
   if (g.n_kh >= CIT_KH_MAX || g.kh_fill + n > CIT_KH_POOL) { g.err |= CIT_ERR_OVERFLOW; return; }
   CitKH& e = g.kh[g.n_kh++];
   e.owner = (uint8_t)owner;
@@ -636,7 +747,7 @@ CIT_HD void cit_init_game(CitGame& g, CitMT& rng, bool preset) {
     const uint64_t kHands[6] = {0x131211100000ull, 0x171615140101ull, 0x1b1a19180302ull,
                                 0x1f1e1d1c0403ull, 0x232221200004ull, 0x002725240100ull};
     for (int p = 0; p < CIT_NP; p++)
-      for (int k = 0; k < 6; k++) put_card(g, HAND(g.pl[p]), deck_take_like(g, (int)((kHands[p] >> (8 * k)) & 0xFF)));
+      for (int k = 0; k < 6; k++) pl_put(g, g.pl[p], AL_HAND, deck_take_like(g, (int)((kHands[p] >> (8 * k)) & 0xFF)));
     g.pl[3].flags |= PF_CROWN;
     // Witch, Spy, Wizard, King, Abbot, Alchemist, Navigator, Warlord (game.py:479-486)
     const uint64_t kRoles = 0x1513100d09070401ull;
@@ -644,7 +755,7 @@ CIT_HD void cit_init_game(CitGame& g, CitMT& rng, bool preset) {
     for (int i = 0; i < CIT_NP; i++) g.turn[i] = (uint8_t)i;
   } else {
     for (int k = 0; k < 4; k++)
-      for (int p = 0; p < CIT_NP; p++) put_card(g, HAND(g.pl[p]), deck_draw(g));
+      for (int p = 0; p < CIT_NP; p++) pl_put(g, g.pl[p], AL_HAND, deck_draw(g));
     for (int r = 0; r < 8; r++) g.roles[r] = (uint8_t)(r * 3 + (int)mt_randbelow(rng, 3));
     for (int i = 0; i < CIT_NP; i++) g.turn[i] = (uint8_t)i;
     shuffle_arr(rng, g.turn, CIT_NP);
@@ -1020,9 +1131,12 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
           for (int su = 0; su < 5; su++) EMIT(mk(O_SPY, a, p, su));
       return false;
     case R_MAGICIAN: {
+      int n = P.n_hand;
+      // hand-slot masks are 64-bit and binom() exact to n = 60; the reference
+      // lists all 2^n - 1 combinations here (itertools), ~1e18 at n = 60
+      if (n > CIT_HAND_MASK_MAX) { s.err |= CIT_ERR_UNSUPPORTED; return true; }
       for (int p = 0; p < CIT_NP; p++)
         if (p != a) EMIT(mk(O_MAGIC_HAND_CHANGE, a, p));
-      int n = P.n_hand;
       for (int r = 1; r <= n; r++) {
         long C = binom(n, r), st = subsample_stride(C);
         int cnt = (int)((C + st - 1) / st);
@@ -1059,6 +1173,7 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
     case R_CARDINAL: {
       bool factory_owned = p_has(P, 35);
       int n = P.n_hand;
+      if (n > CIT_HAND_MASK_MAX) { s.err |= CIT_ERR_UNSUPPORTED; return true; }   // as the magician's
       for (int p = 0; p < CIT_NP; p++) {
         const CitPlayer& Q = g.pl[p];
         for (int i = 0; i < n; i++) {
@@ -1071,7 +1186,7 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
           int k = Q.gold - cost;
           if (k < 0) k = 0;
           if (n - 1 < k) continue;
-          uint8_t slot[CIT_HAND_CAP];
+          uint8_t slot[CIT_HAND_MASK_MAX];
           int m = 0;
           for (int j = 0; j < n; j++)
             if (card_type(P.hand[j]) != t) slot[m++] = (uint8_t)j;
@@ -1326,27 +1441,32 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
         EMIT(mk(O_GOLD_OR_CARD, a, -1, 0));
         if (g.n_deck > 1) EMIT(mk(O_GOLD_OR_CARD, a, -1, 1));
         return false;
-      case 2:
+      case 2: {
+        const uint8_t* jd = pl_jd(P);
+        const int nj = P.n_jd;
         if (p_has(P, 20)) {
-          for (int i = 0; i < P.n_jd; i++)
-            for (int j = i + 1; j < P.n_jd; j++) EMIT(mk(O_WHICH_CARD, a, -1, P.jd[i], P.jd[j], 0, OF_TUPLE));
-        } else {
+          for (int i = 0; i < nj; i++)
+            for (int j = i + 1; j < nj; j++) EMIT(mk(O_WHICH_CARD, a, -1, jd[i], jd[j], 0, OF_TUPLE));
+          return false;
+        }
 #if CIT_WAVE
-          int i = cit_lane(), nj = P.n_jd;
-          int c = i < nj ? P.jd[i] : 0;
+        if (nj <= 64) {
+          int i = cit_lane();
+          int c = i < nj ? jd[i] : 0;
           WEMIT(cit_first_key(i < nj, card_type(c)), mk(O_WHICH_CARD, a, -1, c, CIT_NO_CARD));
-#else
-          uint64_t seen = 0;
-          for (int i = 0; i < P.n_jd; i++) {
-            int t = card_type(P.jd[i]);
-            if (!((seen >> t) & 1)) {
-              seen |= 1ull << t;
-              EMIT(mk(O_WHICH_CARD, a, -1, P.jd[i], CIT_NO_CARD));
-            }
-          }
+          return false;
+        }
 #endif
+        uint64_t seen = 0;
+        for (int i = 0; i < nj; i++) {
+          int t = card_type(jd[i]);
+          if (!((seen >> t) & 1)) {
+            seen |= 1ull << t;
+            EMIT(mk(O_WHICH_CARD, a, -1, jd[i], CIT_NO_CARD));
+          }
         }
         return false;
+      }
       case 3:
         if (bew) { s.err |= CIT_ERR_KEY; return true; }
         if (rp_blackmail(g.rp[rk])) {
@@ -1419,7 +1539,7 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
 //    which consume the game's CPython stream inside get_options; the drawn
 //    permutations go to `seer` (CIT_SEER_MAX packed options per lane:
 //    card i in byte i, handout count in byte 7).
-#define CIT_SEER_MAX (5 * CIT_HAND_CAP * 3)
+#define CIT_SEER_MAX (5 * CIT_AREA_CAP * 3)
 CIT_HD void cit_prepare_options(CitGame& g, CitMT& rng, uint64_t* seer) {
   g.n_sch = 0;
   if ((g.gs_state != 9 && g.gs_state != 8) || g.gs_pid < 0) return;
@@ -1433,7 +1553,7 @@ CIT_HD void cit_prepare_options(CitGame& g, CitMT& rng, uint64_t* seer) {
     for (int pos = 0; pos < k; pos++) {
       for (int j = 0; j < n; j++) {
         int card = P.hand[j], t = card_type(card);
-        uint8_t rest[CIT_HAND_CAP];
+        uint8_t rest[CIT_AREA_CAP];
         int m = 0;
         for (int q = 0; q < n; q++)
           if (card_type(P.hand[q]) != t) rest[m++] = P.hand[q];
@@ -1469,11 +1589,15 @@ CIT_HD void cit_prepare_options(CitGame& g, CitMT& rng, uint64_t* seer) {
 
 // Whether the enumeration of g may raise after it has emitted options: only
 // the blackmailer's character options raise late (gen_role: a possessed rank
-// outside 2..7 after the build options were listed); every other error of
+// outside 2..7 after the build options were listed), and the magician's and
+// cardinal's over a hand past CIT_HAND_MASK_MAX; every other error of
 // cit_enum_options comes before the first option of its branch.
 CIT_HD bool cit_enum_late_error(const CitGame& g) {
   int a = g.gs_pid;
-  return a >= 0 && a < CIT_NP && g.pl[a].role == R_BLACKMAILER;
+  if (a < 0 || a >= CIT_NP) return false;
+  const int role = g.pl[a].role;
+  return role == R_BLACKMAILER ||
+         ((role == R_MAGICIAN || role == R_CARDINAL) && g.pl[a].n_hand > CIT_HAND_MASK_MAX);
 }
 
 CIT_HD int cit_count_options(const CitGame& g, uint32_t& err, const uint64_t* seer) {
@@ -1524,7 +1648,7 @@ CIT_HD void move_crown(CitGame& g, int t) {
 // carry_out_building (option_functions.py:102-127)
 CIT_HD void do_build(CitGame& g, int a, int card, int replica) {
   CitPlayer& P = g.pl[a];
-  put_card(g, BUILD(P), take_like(P.hand, P.n_hand, card));
+  put_card(g, BUILD(P), pl_take_like(g, P, AL_HAND, card));
   if (P.role != R_ALCHEMIST) P.gold = (int16_t)(P.gold - card_cost(card));
   if (replica) P.replicas = (int8_t)replica;
   gs_append(g, card_suit(card) == SUIT_TRADE ? ADM_TRADE : ADM_NON_TRADE);
@@ -1547,9 +1671,9 @@ CIT_HD void settle(CitGame& g, int name, int a, int t, int card) {
   if (ty == 34) {
     int n = T.n_museum;
     for (int i = 0; i < n; i++) {
-      int c = pop_front(T.museum, T.n_museum);
+      int c = pl_pop_front(g, T, AL_MUSEUM);
       if (name == O_WARLORD) put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, c);
-      else put_card(g, MUSEUM(P), c);
+      else pl_put(g, P, AL_MUSEUM, c);
     }
   }
   if (ty == 29 && (T.flags & PF_LIGHTHOUSE)) {
@@ -1565,7 +1689,7 @@ CIT_HD int do_finish(CitGame& g, const CitOpt& o, CitMT& rng) {
   bool dead = rp_of(g, P.role) & RP_DEAD;
   if (g.err) return -1;
   if (!dead && P.n_hand == 0) {     // (the reference tests the building first; both tests are pure)
-    if (p_has(P, 28) && P.n_hand == 0) draw_into(g, rng, JD(P), 2);
+    if (p_has(P, 28) && P.n_hand == 0) pl_draw(g, rng, P, AL_JD, 2);
     if (p_has(P, 30) && P.n_hand == 0) P.gold++;
   }
   if (o.flags & OF_CROWN) {
@@ -1648,31 +1772,31 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
         P.gold += 2;
         gs_set(g, 3, a);
       } else {
-        draw_into(g, rng, JD(P), p_has(P, 16) ? 3 : 2);
+        pl_draw(g, rng, P, AL_JD, p_has(P, 16) ? 3 : 2);
         gs_set(g, 2, a);
       }
       break;
     }
     case O_WHICH_CARD: {                                     // :58-66
-      put_card(g, HAND(P), take_like(P.jd, P.n_jd, o.a));
-      if (o.b != CIT_NO_CARD) put_card(g, HAND(P), take_like(P.jd, P.n_jd, o.b));
+      pl_put(g, P, AL_HAND, pl_take_like(g, P, AL_JD, o.a));
+      if (o.b != CIT_NO_CARD) pl_put(g, P, AL_HAND, pl_take_like(g, P, AL_JD, o.b));
 #if CIT_WAVE
       {
         int i = cit_lane(), nj = P.n_jd, nd = g.n_deck;
         if (nj <= 64 && nd + nj <= CIT_DECK_CAP - 1) {   // no overflow: one store by all lanes
-          int c = i < nj ? P.jd[i] : CIT_NO_CARD;
+          int c = i < nj ? pl_jd(P)[i] : CIT_NO_CARD;
           bool v = i < nj && c != CIT_NO_CARD;
           uint64_t m = cit_ballot(v);
           if (v) deck_ref(g, nd + cit_lane_rank(m)) = (uint8_t)c;
           g.n_deck = (uint8_t)(nd + __popcll(m));
-          P.n_jd = 0;
+          pl_clear(g, P, AL_JD);
           gs_set(g, 3, a);
           break;
         }
       }
 #endif
-      for (int i = 0; i < P.n_jd; i++) deck_put(g, P.jd[i]);
-      P.n_jd = 0;
+      for (int i = 0; i < P.n_jd; i++) deck_put(g, pl_jd(P)[i]);
+      pl_clear(g, P, AL_JD);
       gs_set(g, 3, a);
       break;
     }
@@ -1722,11 +1846,11 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       break;
     case O_SMITHY:                                           // :131-138
       P.gold -= 2;
-      draw_into(g, rng, JD(P), 3);
+      pl_draw(g, rng, P, AL_JD, 3);
       at5(g, a, ADM_SMITHY);
       break;
     case O_LAB:                                              // :140-145
-      put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, take_like(P.hand, P.n_hand, o.a));
+      put_card(g, g.discard, g.n_discard, CIT_DISCARD_CAP, pl_take_like(g, P, AL_HAND, o.a));
       P.gold++;
       at5(g, a, ADM_LAB);
       break;
@@ -1744,13 +1868,13 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
     }
     case O_LIGHTHOUSE:                                       // :173-180
       kh_append(g, a, -1, 5, false, g.n_deck, [&g](int i) { return deck_at(g, i); });
-      put_card(g, HAND(P), deck_take_like(g, o.a));
+      pl_put(g, P, AL_HAND, deck_take_like(g, o.a));
       P.flags &= (uint8_t)~PF_LIGHTHOUSE;
       deck_shuffle(g, rng);
       at5(g, a, -1);
       break;
     case O_MUSEUM:                                           // :161-165
-      put_card(g, MUSEUM(P), take_like(P.hand, P.n_hand, o.a));
+      pl_put(g, P, AL_MUSEUM, pl_take_like(g, P, AL_HAND, o.a));
       at5(g, a, ADM_MUSEUM);
       break;
     case O_GRAVEYARD:                                        // :183-187
@@ -1793,29 +1917,40 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       int steal = n < T.gold ? n : T.gold;
       P.gold = (int16_t)(P.gold + steal);
       T.gold = (int16_t)(T.gold - steal);
-      draw_into(g, rng, HAND(P), 1);
+      pl_draw(g, rng, P, AL_HAND, 1);
       at5(g, a, ADM_ABILITY);
       break;
     }
     case O_MAGIC_HAND_CHANGE: {                              // :291-303
       CitPlayer& T = g.pl[o.target];
-      uint8_t tmp[CIT_HAND_CAP];
-      int n = P.n_hand;
-      for (int i = 0; i < n; i++) tmp[i] = P.hand[i];
-      for (int i = 0; i < T.n_hand; i++) P.hand[i] = T.hand[i];
-      P.n_hand = T.n_hand;
-      for (int i = 0; i < n; i++) T.hand[i] = tmp[i];
-      T.n_hand = (uint8_t)n;
+      const int np = P.n_hand, nt = T.n_hand;
+#if CIT_WAVE
+      {   // lane l holds both hands' cards l and l + 64 (area_splice calls src(l), src(l + 64) on lane l)
+        const int l = cit_lane();
+        const int p0 = l < np ? P.hand[l] : 0, p1 = l + 64 < np ? P.hand[l + 64] : 0;
+        const int t0 = l < nt ? T.hand[l] : 0, t1 = l + 64 < nt ? T.hand[l + 64] : 0;
+        area_splice(g, P, AL_HAND, 0, np, nt, [t0, t1](int i) { return i < 64 ? t0 : t1; });
+        area_splice(g, T, AL_HAND, 0, nt, np, [p0, p1](int i) { return i < 64 ? p0 : p1; });
+      }
+#else
+      {
+        uint8_t hp[CIT_AREA_CAP], ht[CIT_AREA_CAP];
+        for (int i = 0; i < np; i++) hp[i] = P.hand[i];
+        for (int i = 0; i < nt; i++) ht[i] = T.hand[i];
+        area_splice(g, P, AL_HAND, 0, np, nt, [&ht](int i) { return ht[i]; });
+        area_splice(g, T, AL_HAND, 0, nt, np, [&hp](int i) { return hp[i]; });
+      }
+#endif
       at5(g, a, ADM_ABILITY);
       break;
     }
     case O_DISCARD_AND_DRAW: {                               // :291-303, iterate-while-remove
       int i = 0;
       while (i < P.n_hand) {
-        deck_put(g, take_like(P.hand, P.n_hand, P.hand[i]));
+        deck_put(g, pl_take_like(g, P, AL_HAND, P.hand[i]));
         i++;
       }
-      draw_into(g, rng, HAND(P), P.n_hand);
+      pl_draw(g, rng, P, AL_HAND, P.n_hand);
       at5(g, a, ADM_ABILITY);
       break;
     }
@@ -1842,7 +1977,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
         if (g.kh[i].owner == a && (g.kh[i].conf_flags & 0x10)) { e = i; break; }
 #endif
       if (e < 0) { g.err |= CIT_ERR_ATTR; break; }
-      put_card(g, HAND(P), take_like(T.hand, T.n_hand, o.a));
+      pl_put(g, P, AL_HAND, pl_take_like(g, T, AL_HAND, o.a));
       if (o.flags & OF_BUILD) {
         int rep = count_type(P.build, P.n_build, card_type(o.a));   // option.attributes['replica'] is overwritten
         do_build(g, a, o.a, rep);
@@ -1858,7 +1993,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
         if (p == a || !Q.n_hand) continue;
         shuffle_arr(rng, Q.hand, Q.n_hand);
         reshuffle_if_empty(g, rng);
-        put_card(g, HAND(P), pop_front(Q.hand, Q.n_hand));
+        pl_put(g, P, AL_HAND, pl_pop_front(g, Q, AL_HAND));
         g.seer_from[g.n_seer++] = (uint8_t)p;
       }
       gs_set(g, 8, a);
@@ -1871,7 +2006,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       for (int i = 0; i < k; i++) {
         int pid = g.seer_from[i];
         int c = (int)((o.x >> (8 * i)) & 0xFF);
-        put_card(g, HAND(g.pl[pid]), take_like(P.hand, P.n_hand, c));
+        pl_put(g, g.pl[pid], AL_HAND, pl_take_like(g, P, AL_HAND, c));
         kh_append(g, a, pid, 5, false, 1, [c](int) { return c; });
       }
       g.n_seer = 0;
@@ -1885,7 +2020,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       break;
     case O_TAKE_CROWN_PAT: {                                 // :365-375
       int n = count_suit(P.build, P.n_build, SUIT_LORD);
-      draw_into(g, rng, HAND(P), n);
+      pl_draw(g, rng, P, AL_HAND, n);
       if (!(P.flags & PF_WITCH)) move_crown(g, a);
       at5(g, a, ADM_ABILITY);
       break;
@@ -1895,7 +2030,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       P.gold = (int16_t)(P.gold + count_suit(P.build, P.n_build, SUIT_LORD));
       if (o.a == 0) {
         shuffle_arr(rng, T.hand, T.n_hand);
-        put_card(g, HAND(P), pop_front(T.hand, T.n_hand));
+        pl_put(g, P, AL_HAND, pl_pop_front(g, T, AL_HAND));
       } else if (o.a == 1) {
         P.gold++;
         T.gold--;
@@ -1911,24 +2046,24 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       break;
     case O_CARDINAL: {                                       // :422-439
       CitPlayer& T = g.pl[o.target];
-      uint8_t give[CIT_HAND_CAP];
+      uint8_t give[CIT_HAND_MASK_MAX];
       int ng = 0;
-      for (int i = 0; i < P.n_hand; i++)
+      for (int i = 0; i < P.n_hand && i < CIT_HAND_MASK_MAX; i++)
         if ((o.x >> i) & 1) give[ng++] = P.hand[i];
-      put_card(g, BUILD(P), take_like(P.hand, P.n_hand, o.a));
+      put_card(g, BUILD(P), pl_take_like(g, P, AL_HAND, o.a));
       P.gold = (int16_t)(P.gold - (card_cost(o.a) - (o.flags & OF_FACTORY ? 1 : 0)));
       if (P.gold < 0) P.gold = 0;
       if ((int8_t)o.c) P.replicas = (int8_t)o.c;
       if (ng) {
         T.gold = (int16_t)(T.gold - ng);
-        for (int i = 0; i < ng; i++) put_card(g, HAND(T), take_like(P.hand, P.n_hand, give[i]));
+        for (int i = 0; i < ng; i++) pl_put(g, T, AL_HAND, pl_take_like(g, P, AL_HAND, give[i]));
       }
       at5(g, a, ADM_ABILITY);
       break;
     }
     case O_ABBOT_GOLD_OR_CARD:                               // :405-412
       P.gold = (int16_t)(P.gold + (o.a - o.b));
-      draw_into(g, rng, HAND(P), o.b);
+      pl_draw(g, rng, P, AL_HAND, o.b);
       at5(g, a, ADM_ABILITY);
       break;
     case O_ABBOT_BEG: {                                      // :414-420
@@ -1961,11 +2096,11 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       at5(g, a, ADM_ABILITY);
       break;
     case O_ARCHITECT:                                        // :464-471
-      draw_into(g, rng, HAND(P), 2);
+      pl_draw(g, rng, P, AL_HAND, 2);
       at5(g, a, ADM_ABILITY);
       break;
     case O_NAVIGATOR:                                        // :473-483
-      if (o.a == 1) draw_into(g, rng, HAND(P), 4);
+      if (o.a == 1) pl_draw(g, rng, P, AL_HAND, 4);
       else P.gold += 4;
       at5(g, a, ADM_ABILITY);
       break;
@@ -1976,7 +2111,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       for (int i = 0; i < n; i++) {
         reshuffle_if_empty(g, rng);
         int c = deck_draw(g);
-        put_card(g, HAND(P), c);
+        pl_put(g, P, AL_HAND, c);
         put_card(g, g.seven, g.n_seven, CIT_SEVEN_CAP, c);
       }
       gs_set(g, 9, a);
@@ -1985,7 +2120,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       break;
     }
     case O_SCHOLAR_PICK:                                     // :498-502
-      for (int i = 0; i < g.n_seven; i++) deck_put(g, take_like(P.hand, P.n_hand, g.seven[i]));
+      for (int i = 0; i < g.n_seven; i++) deck_put(g, pl_take_like(g, P, AL_HAND, g.seven[i]));
       gs_goto_next(g);
       g.seven_kind = 2;
       g.n_seven = 0;
@@ -2107,9 +2242,14 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
   __syncthreads();
   for (int pass = 0; pass < 2; pass++) {
     int p = pass * 4 + (l >> 4), i = l & 15;
-    if (p < CIT_NP) {
-      if (i < g.pl[p].n_build) atomicAdd(&kt[card_type(g.pl[p].build[i])], 1u);
-      if (i < g.pl[p].n_museum) atomicAdd(&kt[card_type(g.pl[p].museum[i])], 1u);
+    if (p < CIT_NP && i < g.pl[p].n_build) atomicAdd(&kt[card_type(g.pl[p].build[i])], 1u);
+  }
+  {   // museums (any length): the seats holding one, 64 cards per pass
+    const int pl = l < CIT_NP ? l : 0;
+    for (uint64_t m = cit_ballot(l < CIT_NP && g.pl[pl].n_museum > 0); m; m &= m - 1) {
+      const CitPlayer& M = g.pl[__ffsll((unsigned long long)m) - 1];
+      const uint8_t* mu = pl_museum(M);
+      for (int i = l; i < M.n_museum; i += 64) atomicAdd(&kt[card_type(mu[i])], 1u);
     }
   }
   if (l < PC.n_hand) atomicAdd(&kt[card_type(PC.hand[l])], 1u);
@@ -2218,12 +2358,15 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
         n -= kk;
       }
       int m = n < nu - head ? n : nu - head;
-      int nh = wave_append([&Q](int i) -> uint8_t& { return Q.hand[i & (CIT_HAND_CAP - 1)]; }, 0, kk + m,
+      // the new hand overwrites the old one in place (it is never longer: the
+      // unknown cards may run out); a shorter hand pulls the lists after it in
+      const int n_old = Q.n_hand;
+      int nh = wave_append([&Q](int i) -> uint8_t& { return Q.hand[i < CIT_AREA_CAP ? i : 0]; }, 0, kk + m,
                            [&g, unk, ho, kk, head](int i) {
                              return i < kk ? (int)g.kh_pool[ho + i] : (int)unk[head + i - kk];
                            });
       head += m;
-      Q.n_hand = (uint8_t)nh;
+      if (nh < n_old) area_splice(g, Q, AL_HAND, nh, n_old - nh, 0, [](int) { return 0; });
     }
     // sample_roles_for_opponent (:283-295)
     if (role_sample && p != orig && p != g.gs_pid && g.gs_state != 0) {
@@ -2285,7 +2428,7 @@ CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rn
   for (int p = 0; p < CIT_NP; p++)
     for (int i = 0; i < g.pl[p].n_build; i++) kt[card_type(g.pl[p].build[i])]++;
   for (int p = 0; p < CIT_NP; p++)
-    for (int i = 0; i < g.pl[p].n_museum; i++) kt[card_type(g.pl[p].museum[i])]++;
+    for (int i = 0; i < g.pl[p].n_museum; i++) kt[card_type(pl_museum(g.pl[p])[i])]++;
   for (int i = 0; i < PC.n_hand; i++) kt[card_type(PC.hand[i])]++;
   {
     int off = 0;
@@ -2356,13 +2499,18 @@ CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rn
         if (k.owner == orig && k.target == p && (k.conf_flags & 0x20)) { ho = off; hl = k.len; break; }
         off += k.len;
       }
-      Q.n_hand = 0;
+      // the new hand overwrites the old one in place (never longer: the
+      // unknown cards may run out, add_card drops "Deck Empty"); a shorter
+      // hand pulls the lists after it in
+      const int n_old = n;
+      int w = 0;
       if (ho >= 0) {
         int kk = hl < n ? hl : n;
-        for (int i = 0; i < kk; i++) put_card(g, HAND(Q), g.kh_pool[ho + i]);
+        for (int i = 0; i < kk; i++) Q.hand[w++] = g.kh_pool[ho + i];
         n -= kk;
       }
-      for (int i = 0; i < n; i++) put_card(g, HAND(Q), head < nu ? unk[head++] : CIT_NO_CARD);
+      for (int i = 0; i < n && head < nu; i++) Q.hand[w++] = unk[head++];
+      if (w < n_old) area_splice(g, Q, AL_HAND, w, n_old - w, 0, [](int) { return 0; });
     }
     // sample_roles_for_opponent (:283-295)
     if (role_sample && p != orig && p != g.gs_pid && g.gs_state != 0) {

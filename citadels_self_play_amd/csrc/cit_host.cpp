@@ -18,6 +18,7 @@
 #include <thread>
 #include <vector>
 
+#include "cit_area_test.h"
 #include "cit_cfr.h"
 
 extern "C" {
@@ -25,6 +26,22 @@ extern "C" {
 int cith_game_bytes() { return CIT_GAME_BYTES; }
 int cith_sizeof_game() { return (int)sizeof(CitGame); }
 int cith_seer_max() { return CIT_SEER_MAX; }
+
+// cit_area_test.h's operation sequence on B zeroed games (lane l: seeds[l]),
+// the scalar paths of the card-area list operations; ops[l * n_ops + i] logs
+// op i.  Returns 0.
+int cith_area_test(CitGame* g, int B, const uint64_t* seeds, int n_ops, uint32_t* log) {
+  for (int l = 0; l < B; l++) {
+    CitMT r;
+    r.mt = nullptr;   // never drawn from: the sequence keeps the deck stocked
+    r.stride = 1;
+    r.pos = 0;
+    r.coop = 0;
+    uint64_t s = seeds[l] | 1ull;
+    for (int i = 0; i < n_ops && !g[l].err; i++) area_test_op(g[l], r, s, log + (long)l * n_ops + i);
+  }
+  return 0;
+}
 
 // field offsets, checked against the Python mirror in layout.py
 int cith_layout(int* out, int n) {

@@ -122,6 +122,24 @@ __global__ void k_cfr_choose(uint8_t* pool, int B, int node_cap, int edge_cap, c
   npidx[l] = T.np.pos;
 }
 
+// get_options one game per lane (the per-lane execution model of the
+// enumeration, for parity checks against the wave-uniform k_get_options):
+// rows and streams stay in HBM.
+__global__ void k_get_options_lanes(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t* seer, int B, CitOpt* opts,
+                                    int max_opts, int32_t* n_opts) {
+  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= B) return;
+  CitGame& g = *reinterpret_cast<CitGame*>(games + l * ROW_W);
+  CitMT r = lane_mt(mt, idx, B, l);
+  uint64_t* sc = seer + l * CIT_SEER_MAX;
+  cit_prepare_options(g, r, sc);
+  ListSink s(opts + l * max_opts, max_opts);
+  cit_enum_options(g, s, sc);
+  g.err |= s.err;
+  n_opts[l] = s.n;
+  idx[l] = r.pos;
+}
+
 size_t lds_bytes(int G) { return (size_t)G * LDS_W * 4; }
 
 bool g_attrs_done = false;
@@ -151,6 +169,14 @@ int cit_rollout_lanes(uint32_t* games, uint32_t* mt, uint32_t* mt_idx, uint64_t*
 }
 
 extern "C" {
+
+int cit_get_options_lanes(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, CitOption* opts,
+                          int max_opts, int32_t* n_opts, hipStream_t stream) {
+  if (B <= 0 || max_opts < 0 || !games || !mt || !mt_idx || !seer || !n_opts || (max_opts && !opts)) return -1;
+  hipLaunchKernelGGL(k_get_options_lanes, dim3((B + 63) / 64), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx,
+                     seer, B, (CitOpt*)opts, max_opts, n_opts);
+  CHECK_LAUNCH();
+}
 
 int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
                          int32_t* counts, hipStream_t stream) {

@@ -63,8 +63,10 @@ def pool_caps(iters):
 
 # Row slots of large trees' node pools: diffs against the tree's base row with
 # room for CFR_ROW_CAP differing dwords (cit_cfr.h; a cfr_train(200000) node
-# differs in ~70 of 388, at most ~100 measured): a node's pool bytes halve, so
-# twice the trees fit in HBM.  A tree with a row past the cap is searched again
+# differs in ~70 of 388, at most ~100 measured): a node's record + row slot
+# go from 1,720 to 744 B (with its edge slots ~1.9 KB -> ~0.94 KB), so about
+# twice the trees fit in HBM (config 5: 688 -> 1,326 queue slots, DESIGN.md
+# §2).  A tree with a row past the cap is searched again
 # with raw rows (_retry_overflow).  Small trees (configs 3/4) keep raw rows.
 CFR_ROW_CAP = int(os.environ.get("CIT_ROW_CAP", "128"))      # (0: raw rows everywhere, for A/B runs)
 # cfr_pred splits batches of at least this many trees into 2 stream groups
@@ -364,6 +366,15 @@ class GameBatch:
         f32, counts [B,2]."""
         d = self.device
         roots = roots.to(device=d, dtype=torch.int32).contiguous()
+        groups = getattr(self, "_groups", None)
+        if groups is not None:                 # a cfr_pred split into stream groups: each sub-batch holds its trees
+            parts, subs = groups
+            outs = []
+            for lanes, sub in zip(parts, subs):
+                outs.append(sub.cfr_targets(roots[lanes].clone(), mode))
+                self.mt[:, lanes] = sub.mt
+                self.mt_idx[lanes] = sub.mt_idx
+            return _merge_parts(outs, parts, self.B)
         retry = getattr(self, "_retry", None)
         if retry is not None:
             over, sub = retry
@@ -379,6 +390,8 @@ class GameBatch:
 
     def _cfr_targets(self, roots, mode):
         d = self.device
+        if getattr(self, "_groups", None) is not None:
+            raise RuntimeError("the last search ran in stream groups: its trees are in the sub-batches")
         if mode == 0 and getattr(self, "_model_tree", True) is False:
             mode = 2                                  # CFR_TGT_PRUNE: searched without a model
 
@@ -460,6 +473,8 @@ class GameBatch:
     def arena_used(self):
         """(node blocks, edge blocks) handed out by the last search's arena and its
         capacity (node, edge); a count above capacity means it ran out."""
+        if getattr(self, "_groups", None) is not None:
+            raise RuntimeError("the last search ran in stream groups: see the sub-batches' arena_used()")
         off = self.B * self.lib.cit_cfr_pool_bytes(self.node_cap, self.edge_cap)
         h = self.pool[off:off + 16].cpu().numpy().view("<u4")
         return (int(h[0]), int(h[2])), (int(h[1]), int(h[3]))
@@ -690,6 +705,37 @@ class GameBatch:
 
     def terminal(self):
         return self.games[:, L.CitGame.terminal.offset].to(torch.bool)
+
+
+def _merge_parts(outs, parts, B):
+    """cfr_targets of sub-batches (sub lane i of part g = global lane parts[g][i])
+    -> one dict in global lane order (see _merge_targets)."""
+    d = outs[0]["meta"].device
+    metas, firsts, feats, values, dists, opts = [], [], [], [], [], []
+    counts = torch.zeros((B, 2), dtype=torch.int32, device=d)
+    base = 0
+    for out, lanes in zip(outs, parts):
+        lanes = lanes.to(d)
+        m = out["meta"].clone()
+        m[:, 0] = lanes[m[:, 0].long()].to(m.dtype)
+        metas.append(m)
+        firsts.append(out["meta"][:, 4].long() + base)
+        base += out["dist"].shape[0]
+        feats.append(out["feat"])
+        values.append(out["value"])
+        dists.append(out["dist"])
+        opts.append(out["opt_feat"])
+        counts[lanes] = out["counts"]
+    meta = torch.cat(metas)
+    order = torch.sort(meta[:, 0].long() * (1 << 32) + torch.arange(meta.shape[0], device=d), stable=True).indices
+    meta = meta[order]
+    first = torch.cat(firsts)[order]
+    nch = meta[:, 3].long()
+    new_first = torch.cumsum(nch, 0) - nch
+    rows = torch.repeat_interleave(first - new_first, nch) + torch.arange(int(nch.sum()), device=d)
+    meta[:, 4] = new_first.to(meta.dtype)
+    return {"meta": meta, "feat": torch.cat(feats)[order], "value": torch.cat(values)[order],
+            "dist": torch.cat(dists)[rows], "opt_feat": torch.cat(opts)[rows], "counts": counts}
 
 
 def _merge_targets(main, extra, over):

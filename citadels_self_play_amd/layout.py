@@ -7,12 +7,12 @@ two definitions cannot drift apart silently.
 import ctypes as C
 
 NP = 6
-HAND_CAP, BUILD_CAP, JD_CAP, MUSEUM_CAP = 32, 16, 40, 16
-DECK_CAP, DISCARD_CAP, USED_CAP = 128, 80, 80
-KH_MAX, KH_POOL, SEVEN_CAP = 32, 252, 8
+AREA_CAP, BUILD_CAP = 88, 16     # a player's hand | just_drawn | museum share AREA_CAP slots
+DECK_CAP, DISCARD_CAP, USED_CAP = 128, 88, 80
+KH_MAX, KH_POOL, SEVEN_CAP = 32, 244, 8
 GAME_BYTES = 1552
 MT_N = 624
-SEER_MAX = 5 * HAND_CAP * 3      # CIT_SEER_MAX: packed seer give-back options per lane
+SEER_MAX = 5 * AREA_CAP * 3      # CIT_SEER_MAX: packed seer give-back options per lane
 NO_CARD = 255
 ROLE_BEWITCHED, ROLE_NONE = 27, 255
 
@@ -23,13 +23,23 @@ ERR_BITS = {
 
 
 class CitPlayer(C.Structure):
+    """`hand` is the player's card area: the hand at [0, n_hand), then the
+    just-drawn cards and the museum (the `jd` / `museum` properties)."""
     _fields_ = [
-        ("hand", C.c_uint8 * HAND_CAP), ("build", C.c_uint8 * BUILD_CAP), ("jd", C.c_uint8 * JD_CAP),
-        ("museum", C.c_uint8 * MUSEUM_CAP),
+        ("hand", C.c_uint8 * AREA_CAP), ("build", C.c_uint8 * BUILD_CAP),
         ("n_hand", C.c_uint8), ("n_build", C.c_uint8), ("n_jd", C.c_uint8), ("n_museum", C.c_uint8),
         ("gold", C.c_int16), ("role", C.c_uint8), ("replicas", C.c_int8), ("flags", C.c_uint8),
         ("pad0", C.c_uint8), ("kr", C.c_uint16 * NP), ("pad1", C.c_uint16),
     ]
+
+    @property
+    def jd(self):
+        return list(self.hand[self.n_hand:self.n_hand + self.n_jd])
+
+    @property
+    def museum(self):
+        o = self.n_hand + self.n_jd
+        return list(self.hand[o:o + self.n_museum])
 
 
 class CitKH(C.Structure):

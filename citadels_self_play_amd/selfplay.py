@@ -497,6 +497,34 @@ def _overflowed(stats):
     return (stats[:, 4] & ERR_OVERFLOW) != 0
 
 
+ERROR_CLASSES = ("value_error", "terminal", "capacity", "pool")
+
+
+def error_classes(stats, terminal):
+    """Per-lane class of a tree that yields no targets (-1: none) and the count
+    of each class, in ERROR_CLASSES order:
+      value_error  the search raised one of the reference's own exceptions
+                   (CIT_ERR_* other than the overflow bit: a ValueError from
+                   np.random.choice over an empty or NaN row, ...);
+      terminal     the position was already over (run_mccfr raises on it);
+      capacity     an engine list overflowed (CIT_ERR_OVERFLOW without a pool
+                   bit): only a player holding more than 88 cards, or more
+                   than 32 hand-knowledge entries, can -- the reference has no
+                   such limit;
+      pool         a node pool still overflowed after its retries."""
+    from .engine import ERR_OVERFLOW, ERR_POOL
+    err = stats[:, 4].cpu()
+    term = terminal.cpu().to(torch.bool)
+    over = (err & ERR_OVERFLOW) != 0
+    pool = over & ((err & ERR_POOL) != 0)
+    cls = torch.full(err.shape, -1, dtype=torch.int64)
+    cls[(err != 0) & ~over] = 0
+    cls[term] = 1
+    cls[over & ~pool & ~term] = 2
+    cls[pool & ~term] = 3
+    return cls, {k: int((cls == i).sum()) for i, k in enumerate(ERROR_CLASSES)}
+
+
 def _roots_for_targets(stats):
     """Root ids for cfr_targets with every lane whose search ended in an error
     set to -1, so it yields no targets: a reference ValueError ends

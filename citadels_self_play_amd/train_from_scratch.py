@@ -24,9 +24,10 @@ ends the run: get_mccfr_targets catches only RanOutOfMemory
 (train_from_scratch.py:56-63).  `--on-error raise` reproduces that (a
 TreeError, a ValueError, on every rank).  The default `drop` keeps going
 without those trees and logs per round how many were dropped and why
-(reference value errors, terminal positions, and capacity overflows that
-no retry fixes, which have no reference counterpart); none of them
-contributes targets.
+(selfplay.error_classes: reference value errors, terminal positions, and
+the engine-only classes -- a player past the 88-slot card area, a node pool
+past its retries -- which raise EngineCapacityError under `raise`); none of
+them contributes targets.
 """
 import argparse
 import os
@@ -45,27 +46,27 @@ class TreeError(ValueError):
     the reference's data generation stops there)."""
 
 
+class EngineCapacityError(RuntimeError):
+    """--on-error raise: a tree hit a limit of this engine that the reference
+    does not have (selfplay.error_classes "capacity" / "pool"), so its targets
+    cannot be reproduced; not a reference exception."""
+
+
 def lane_errors(stats, t, seeds):
-    """Per-round error accounting: (value_errors, overflow, terminal, first
-    failing seed).  `value_errors` are trees that raised one of the reference's
-    exceptions in the search (CIT_ERR_* other than the pool overflow);
-    `overflow` trees hit a fixed capacity the reference does not have (an
-    engine list such as a museum of more than 16 cards, or a node pool after
-    every retry); `terminal` positions were already over (run_mccfr raises on
-    them in the reference)."""
-    from .engine import ERR_OVERFLOW
-    err = stats[:, 4].cpu()
-    term = t["terminal"].cpu()
-    over = (err & ERR_OVERFLOW) != 0
-    value = (err != 0) & ~over & ~term
-    bad = (err != 0) | term
-    first = int(seeds[int(bad.nonzero()[0])]) if bool(bad.any()) else None
-    return int(value.sum()), int(over.sum()), int(term.sum()), first
+    """Per-round error accounting: (counts by selfplay.ERROR_CLASSES, first
+    failing seed of the reference's classes, first seed of the engine's)."""
+    from .selfplay import error_classes
+    cls, counts = error_classes(stats, t["terminal"])
+    ref = ((cls == 0) | (cls == 1)).nonzero().flatten()
+    eng = ((cls == 2) | (cls == 3)).nonzero().flatten()
+    first_ref = int(seeds[int(ref[0])]) if ref.numel() else None
+    first_eng = int(seeds[int(eng[0])]) if eng.numel() else None
+    return counts, first_ref, first_eng
 
 
 def collect(rank, world, args, phase, min_targets, log):
     feats, values, tuples = [], [], []
-    dropped = {"value": 0, "overflow": 0, "terminal": 0}
+    dropped = {k: 0 for k in selfplay.ERROR_CLASSES}
     pooled = 0
     rnd = 0
     while pooled < min_targets:
@@ -73,28 +74,31 @@ def collect(rank, world, args, phase, min_targets, log):
         seeds = selfplay.shard(args.games_per_gpu * world, base_seed=base)
         t0 = time.time()
         b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap, log=log)
-        n_value, n_over, n_term, first = lane_errors(stats, t, seeds)
+        counts, first_ref, first_eng = lane_errors(stats, t, seeds)
         if args.on_error == "raise":
-            bad = torch.tensor([0 if first is None else 1], device=stats.device)
+            bad = torch.tensor([0 if first_ref is None else 1, 0 if first_eng is None else 1], device=stats.device)
             if world > 1:
                 torch.distributed.all_reduce(bad)          # every rank stops together
-            if int(bad.item()):
+            if int(bad[0].item()):
                 raise TreeError("simulate_game raised in the search (first failing seed on this rank: %s; "
-                                "%d value errors, %d terminal positions, %d capacity overflows)"
-                                % (first, n_value, n_term, n_over))
+                                "%d value errors, %d terminal positions)"
+                                % (first_ref, counts["value_error"], counts["terminal"]))
+            if int(bad[1].item()):
+                raise EngineCapacityError("a tree exceeded an engine capacity the reference does not have (first "
+                                          "seed on this rank: %s; %d capacity, %d pool)"
+                                          % (first_eng, counts["capacity"], counts["pool"]))
         f, v = selfplay.all_gather_targets(t["feat"], t["value"])
         feats.append(f.cpu())
         values.append(v.cpu())
         if args.save_tuples:
             tuples += selfplay.targets_to_tuples(t)
         pooled += f.shape[0]
-        dropped["value"] += n_value
-        dropped["overflow"] += n_over
-        dropped["terminal"] += n_term
+        for k in dropped:
+            dropped[k] += counts[k]
         log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), dropped trees on rank %d: %d value "
-            "errors (the reference's ValueError), %d already-terminal positions, %d capacity overflows, %.1fs"
-            % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, rank, n_value, n_term, n_over,
-               time.time() - t0))
+            "errors (the reference's ValueError), %d already-terminal positions, %d engine capacity, %d node pool, "
+            "%.1fs" % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, rank, counts["value_error"],
+                       counts["terminal"], counts["capacity"], counts["pool"], time.time() - t0))
         rnd += 1
     collect.dropped = dropped
     return torch.cat(feats), torch.cat(values), tuples

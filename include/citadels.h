@@ -8,7 +8,10 @@
  * file:line; the Python binding a maintainer would add is in INTEGRATION.md.
  *
  * Data (see citadels_self_play_amd/csrc/cit_core.h for the exact layout):
- *   games  : B rows of cit_game_bytes() bytes, one packed game per row.
+ *   games  : B rows of cit_game_bytes() bytes, one packed game per row.  A
+ *            player's hand, just-drawn cards and museum share one 88-slot card
+ *            area (hand first), so none of the reference's unbounded lists
+ *            overflows before a player holds more cards than a game deals.
  *   mt     : uint32 [624][B] CPython MT19937 words, structure-of-arrays.
  *   mt_idx : uint32 [B] stream positions.  Lane l reproduces the reference run
  *            after `random.seed(seeds[l])`.
@@ -48,10 +51,16 @@ typedef struct CitOption {
   uint64_t x;
 } CitOption;
 
-int cit_abi_version(void);              /* 5: packed value-MLP path (4: node pools with diff row slots) */
+int cit_abi_version(void);              /* 6: per-player card areas (hand / just-drawn / museum share 88 slots); 5: packed value-MLP path */
 int cit_game_bytes(void);              /* row width of `games` */
 int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
 int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
+/* Self-test of the card-area list operations (csrc/cit_area_test.h): lane l
+ * runs a pseudo-random sequence of n_ops list operations (seeds[l]) on its
+ * game row (zeroed by the caller); log[l][i] records op i.  Tests compare the
+ * rows and logs with the host build's. */
+int cit_area_test(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int n_ops,
+                  uint32_t* log, hipStream_t stream);
 
 /* random.seed(seeds[l]) (CPython init_by_array) or, numpy_style != 0,
  * np.random.seed(seeds[l]) (init_genrand) for every lane. */
@@ -78,6 +87,11 @@ int cit_init(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t*
  * (scholar state 9, seer state 8). */
 int cit_get_options(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, CitOption* opts,
                     int max_opts, int32_t* n_opts, hipStream_t stream);
+/* The same, one game per lane (the one-game-per-lane execution model of
+ * cit_rollout_random's games_per_block > 0, compiled without the wave-uniform
+ * list scans): a parity check of the enumeration against cit_get_options. */
+int cit_get_options_lanes(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* seer, int B, CitOption* opts,
+                          int max_opts, int32_t* n_opts, hipStream_t stream);
 
 /* len(Game.get_options_from_state()) for every lane, counted without
  * materialising the list (the random-role cardinal / magician lists run into

@@ -17,7 +17,7 @@ _lib = None
 
 
 def build(force=False):
-    srcs = [os.path.join(SRC, f) for f in ("cit_host.cpp", "cit_engine.h", "cit_core.h", "cit_cfr.h")]
+    srcs = [os.path.join(SRC, f) for f in ("cit_host.cpp", "cit_engine.h", "cit_core.h", "cit_cfr.h", "cit_area_test.h")]
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(s) for s in srcs):
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)

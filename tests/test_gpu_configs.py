@@ -105,7 +105,7 @@ def test_gpu_train_from_scratch_on_error(tmp_path):
     with pytest.raises(ValueError, match="simulate_game raised"):
         T.main(args + ["--on-error", "raise"])
     T.main(args + ["--on-error", "drop"])
-    assert T.collect.dropped["value"] >= 1
+    assert T.collect.dropped["value_error"] >= 1 and T.collect.dropped["capacity"] == 0
 
 
 @pytest.fixture(scope="module")

@@ -144,6 +144,11 @@ struct CfrTree {
   CitOpt* lbuf;                        // CFR_LBUF descriptors (LDS on the device)
   uint32_t err;
   uint32_t carry_outs;
+  // The search's current node (the one cfr_update_strategy last read): its
+  // header fields, so the choice, the step to the chosen child and the
+  // child's expansion (which asks for its parent's player and state) do not
+  // read the record from HBM again.  cur_node -1: nothing cached.
+  int cur_node, cur_fe, cur_nch, cur_flags, cur_player, cur_state;
 };
 
 CIT_HD int cfr_nblocks(int node_cap) { return (node_cap + CFR_NB - 1) >> CFR_NB_SHIFT; }
@@ -186,6 +191,7 @@ CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, int B, long l, int node_cap
   T.edge_base = T.row_base + ncap * CFR_NB * T.row_slot;
   T.node_cap = node_cap;
   T.edge_cap = edge_cap;
+  T.cur_node = -1;
 }
 // Resumable cfr_pred state of one tree (see cfr_pred_run below): 64 B,
 // persists in HBM between launches.
@@ -865,10 +871,27 @@ CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
 }
 
 // ------------------------------------------------------------ expansion
-CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
+// The parent's player and game state for a child's expansion (the
+// determinization rule of expand_for_*: deep_mccfr.py:140,158): the cached
+// current node's when the child was just reached from it.
+CIT_HD void cfr_parent_info(const CfrTree& T, int par, int& player, int& state) {
+  if (par >= 0 && cfr_u(T.cur_node) == par) {
+    player = cfr_u(T.cur_player);
+    state = cfr_u(T.cur_state);
+  } else if (par >= 0) {
+    const CfrNode& P = cfr_node(T, par);
+    player = P.player;
+    state = P.gs_state;
+  } else {
+    player = state = -1;
+  }
+}
+
+CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n, int depth) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(8);            // :102-131
   n = cfr_u(n);
+  depth = cfr_u(depth) + 1;
   int f = alloc_edges(T, CFR_ROLE_EDGE_SLOTS);
   if (f < 0) return;
   CfrWide* W = cfr_wide(T, f);
@@ -876,7 +899,6 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
     for (int k = 0; k < 6; k++) W[r].R[k] = W[r].S[k] = W[r].CS[k] = 0.0;
   cfr_node(T, n).first_edge = f;
   cfr_node(T, n).edge_cap = CFR_ROLE_CHILDREN;
-  int depth = cfr_node(T, n).depth + 1;
   CitGame& h = cfr_w(T, 1);
   for (int r = 0; r < CFR_ROLE_CHILDREN && !T.err; r++) {
     row_load(T, w_row(T, 1), n);
@@ -902,10 +924,17 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n) {
   }
 }
 
-CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
+CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n, int par, int player, int depth) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(9);                   // :133-151
   n = cfr_u(n);
+  par = cfr_u(par);
+  player = cfr_u(player);
+  depth = cfr_u(depth) + 1;
+  int pp, ps;
+  cfr_parent_info(T, par, pp, ps);
+  const bool sample = par < 0 || player != pp;
+  const bool role_sample = par >= 0 && ps != 0;
   CitGame& g = cfr_w(T, 0);
   row_load(T, w_row(T, 0), n);
   eng_prepare(T, 0);
@@ -921,10 +950,6 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
   CfrNode& N = cfr_node(T, n);
   N.first_edge = f;
   N.edge_cap = (int16_t)cnt;
-  int par = N.parent;
-  bool sample = par < 0 || N.player != cfr_node(T, par).player;
-  bool role_sample = par >= 0 && cfr_node(T, par).gs_state != 0;
-  int depth = N.depth + 1;
   const CitOpt* ob = cfr_glb(T.optbuf);
   CitGame& h = cfr_w(T, 1);
   for (int i = 0; i < cnt && !T.err; i++) {
@@ -943,15 +968,20 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n) {
   }
 }
 
-CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
+CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player, int depth, int nch, int fe) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(10);              // :153-179
   n = cfr_u(n);
-  CfrNode& N = cfr_node(T, n);
+  par = cfr_u(par);
+  player = cfr_u(player);
+  depth = cfr_u(depth) + 1;
+  nch = cfr_u(nch);
+  fe = cfr_u(fe);
+  int pp, ps;
+  cfr_parent_info(T, par, pp, ps);
   row_load(T, w_row(T, 1), n);
   CitGame& h = cfr_w(T, 1);
-  int par = N.parent;
-  if (par < 0 || N.player != cfr_node(T, par).player) eng_sample(T, 1, T.orig, par >= 0 && cfr_node(T, par).gs_state != 0);
+  if (par < 0 || player != pp) eng_sample(T, 1, T.orig, par >= 0 && ps != 0);
   eng_prepare(T, 1);
   CfrCnt lc = cfr_ucnt(eng_list_lds(T, 1));
   T.err |= lc.err | h.err;
@@ -963,30 +993,41 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n) {
   eng_carry(T, 1, o);
   T.err |= h.err;
   if (T.err) return;
-  for (int j = 0; j < N.n_children; j++)
-    if (opt_eq((*cfr_edge(T, N.first_edge + j)).opt, key)) return;
-  if (N.first_edge < 0) {
-    int f = alloc_edges(T, CFR_OPP_CHILDREN);
-    if (f < 0) return;
-    N.first_edge = f;
+#if CIT_WAVE
+  if (nch > 0) {   // lane j compares child j's option: one round of loads
+    const int l = CFR_LANE;
+    bool hit = false;
+    if (l < nch) hit = opt_eq((*cfr_edge(T, fe + l)).opt, key);
+    if (__ballot(hit)) return;
+  }
+#else
+  for (int j = 0; j < nch; j++)
+    if (opt_eq((*cfr_edge(T, fe + j)).opt, key)) return;
+#endif
+  if (fe < 0) {
+    fe = alloc_edges(T, CFR_OPP_CHILDREN);
+    if (fe < 0) return;
+    CfrNode& N = cfr_node(T, n);
+    N.first_edge = fe;
     N.edge_cap = CFR_OPP_CHILDREN;
   }
-  int c = cfr_u(cfr_node(T, 1, n, N.depth + 1, 0));
+  int c = cfr_u(cfr_node(T, 1, n, depth, 0));
   if (c < 0) return;
-  init_edge((*cfr_edge(T, cfr_node(T, n).first_edge + cfr_node(T, n).n_children)), key, c);
-  cfr_node(T, c).sib = cfr_node(T, n).n_children;
-  cfr_node(T, n).n_children++;
+  init_edge((*cfr_edge(T, fe + nch)), key, c);
+  cfr_node(T, c).sib = (int16_t)nch;
+  cfr_node(T, n).n_children = (int16_t)(nch + 1);
 }
 
 CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
   CfrNode& N = cfr_node(T, n);
-  if (N.gs_state == 0 && N.n_children == 0) {
+  const int state = N.gs_state, nch = N.n_children, player = N.player, par = N.parent, depth = N.depth;
+  if (state == 0 && nch == 0) {
     N.flags |= NF_ROLE_PICK;
-    cfr_expand_role_pick(T, n);
-  } else if (N.player == T.orig && N.n_children == 0) {
-    cfr_expand_own(T, n);
-  } else if (N.player != T.orig && N.n_children < CFR_OPP_CHILDREN) {
-    cfr_expand_opponent(T, n);
+    cfr_expand_role_pick(T, n, depth);
+  } else if (player == T.orig && nch == 0) {
+    cfr_expand_own(T, n, par, player, depth);
+  } else if (player != T.orig && nch < CFR_OPP_CHILDREN) {
+    cfr_expand_opponent(T, n, par, player, depth, nch, N.first_edge);
   }
 }
 
@@ -996,31 +1037,60 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
   CIT_PROF_SCOPE(11);               // :292-319
   n = cfr_u(n);
   CfrNode& N = cfr_node(T, n);
-  int nch = N.n_children;
+  const int nch = N.n_children, fe = N.first_edge, flags = N.flags;
+  T.cur_node = n;
+  T.cur_fe = fe;
+  T.cur_nch = nch;
+  T.cur_flags = flags;
+  T.cur_player = N.player;
+  T.cur_state = N.gs_state;
   if (nch == 0) return;
-  CfrEdge* E = cfr_edge(T, N.first_edge);
+  CfrEdge* E = cfr_edge(T, fe);
 #if CIT_WAVE
-  if (!(N.flags & NF_ROLE_PICK) && nch <= CFR_SBUF && cfr_ls.sbuf_on) {
-    // lane a (a + 64, ...) owns edge a; the numpy sums run in their serial
-    // order over LDS copies (cbuf keeps the normalised CS for cfr_choose)
+  static_assert(CFR_SBUF <= 128, "two edges per lane");
+  if (!(flags & NF_ROLE_PICK) && nch <= CFR_SBUF && cfr_ls.sbuf_on) {
+    // lanes l and l + 64 own edges l and l + 64 (their R and CS loaded in one
+    // round); the numpy sums run in their serial order over LDS copies (cbuf
+    // keeps the normalised CS for cfr_choose)
     double* sb = cfr_ls.sbuf;
     double* cb = cfr_ls.cbuf;
     const int l = CFR_LANE;
-    for (int a = l; a < nch; a += 64) sb[a] = exp((-E[a].R) * CFR_LN13);
+    const bool h0 = l < nch, h1 = l + 64 < nch;
+    double r0 = 0.0, c0 = 0.0, r1 = 0.0, c1 = 0.0;
+    if (h0) {
+      r0 = E[l].R;
+      c0 = E[l].CS;
+    }
+    if (h1) {
+      r1 = E[l + 64].R;
+      c1 = E[l + 64].CS;
+    }
+    if (h0) sb[l] = exp((-r0) * CFR_LN13);
+    if (h1) sb[l + 64] = exp((-r1) * CFR_LN13);
     CFR_SYNC();
     double tot = np_sum([sb](int i) { return sb[i]; }, nch, T.err);
-    for (int a = l; a < nch; a += 64) {
-      double v = tot > 0 ? sb[a] / tot : 1.0 / nch;
-      E[a].S = v;
-      cb[a] = E[a].CS + v;
+    if (h0) {
+      double v = tot > 0 ? sb[l] / tot : 1.0 / nch;
+      E[l].S = v;
+      cb[l] = c0 + v;
+    }
+    if (h1) {
+      double v = tot > 0 ? sb[l + 64] / tot : 1.0 / nch;
+      E[l + 64].S = v;
+      cb[l + 64] = c1 + v;
     }
     CFR_SYNC();
     double cs = np_sum([cb](int i) { return cb[i]; }, nch, T.err);
     CFR_SYNC();
-    for (int a = l; a < nch; a += 64) {
-      double v = cb[a] / cs;
-      E[a].CS = v;
-      cb[a] = v;
+    if (h0) {
+      double v = cb[l] / cs;
+      E[l].CS = v;
+      cb[l] = v;
+    }
+    if (h1) {
+      double v = cb[l + 64] / cs;
+      E[l + 64].CS = v;
+      cb[l + 64] = v;
     }
     CFR_SYNC();
     cfr_ls.cnode = n;
@@ -1029,7 +1099,7 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
   }
   cfr_ls.cnode = -1;
 #endif
-  if (!(N.flags & NF_ROLE_PICK)) {
+  if (!(flags & NF_ROLE_PICK)) {
     for (int a = 0; a < nch; a++) E[a].S = exp((-E[a].R) * CFR_LN13);
     double tot = np_sum([E](int i) { return E[i].S; }, nch, T.err);
     for (int a = 0; a < nch; a++) E[a].S = tot > 0 ? E[a].S / tot : 1.0 / nch;
@@ -1038,7 +1108,7 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
     for (int a = 0; a < nch; a++) E[a].CS = E[a].CS / cs;
   } else {
     // role pick: [6 players, nch] arrays; totals along players (axis 0, sequential)
-    CfrWide* W = cfr_wide(T, N.first_edge);
+    CfrWide* W = cfr_wide(T, fe);
     double tots[CFR_ROLE_CHILDREN];
     bool small = false;
     for (int a = 0; a < nch; a++) {
@@ -1068,10 +1138,19 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(12);
   n = cfr_u(n);
-  CfrNode& N = cfr_node(T, n);
-  int nch = N.n_children;
-  const CfrEdge* E = cfr_edge(T, N.first_edge < 0 ? 0 : N.first_edge);
-  if (!(N.flags & NF_ROLE_PICK)) {
+  int nch, fe, flags;
+  if (cfr_u(T.cur_node) == n) {            // cfr_update_strategy(n) read the header
+    nch = cfr_u(T.cur_nch);
+    fe = cfr_u(T.cur_fe);
+    flags = cfr_u(T.cur_flags);
+  } else {
+    const CfrNode& N = cfr_node(T, n);
+    nch = N.n_children;
+    fe = N.first_edge;
+    flags = N.flags;
+  }
+  const CfrEdge* E = cfr_edge(T, fe < 0 ? 0 : fe);
+  if (!(flags & NF_ROLE_PICK)) {
 #if CIT_WAVE
     if (cfr_ls.cnode == n && cfr_ls.cnch == nch) {   // update_strategy(n) left CS in LDS
       const double* cb = cfr_ls.cbuf;
@@ -1082,7 +1161,7 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
     double tot = np_sum([E](int i) { return E[i].CS; }, nch, T.err);
     return np_choice(T.np, [E, tot](int i) { return E[i].CS / tot; }, nch, T.err);
   }
-  const CfrWide* W = cfr_wide(T, N.first_edge);
+  const CfrWide* W = cfr_wide(T, fe);
   // weighted_average_strategy (:51-65) over turn_orders_for_roles of the node's game
   const CitGame& g = row_view(T, n, 1);
   if (nch > CFR_ROLE_CHILDREN) { T.err |= CIT_ERR_OVERFLOW; return -1; }
@@ -1100,21 +1179,24 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
 }
 
 // ------------------------------------------------------------- backup
-CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
+// (the node's header fields come from the caller's read of its record)
+CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n, int nch, int fe, int flags, int player) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(13);                // :231-256
   n = cfr_u(n);
-  CfrNode& N = cfr_node(T, n);
-  CfrEdge* E = cfr_edge(T, N.first_edge);
-  int nch = N.n_children;
+  nch = cfr_u(nch);
+  fe = cfr_u(fe);
+  flags = cfr_u(flags);
+  player = cfr_u(player);
+  CfrEdge* E = cfr_edge(T, fe);
 #if CIT_WAVE
   if (nch <= 64) {
     // lane a reads child a (one round of loads for all children); the max runs
     // in the serial order over the lanes' values, so NaN / tie handling and
     // every sum are the serial loop's
     const int a = CFR_LANE;
-    if (!(N.flags & NF_ROLE_PICK)) {
-      int p = N.player;
+    if (!(flags & NF_ROLE_PICK)) {
+      int p = player;
       double v = a < nch ? cfr_node(T, E[a].child).wp[p] : 0.0;
       double mx = cfr_readlane_f64(v, 0);
       for (int k = 1; k < nch; k++) {
@@ -1123,7 +1205,7 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
       }
       if (a < nch) E[a].R += mx - v;
     } else if (a < nch) {
-      CfrWide& W = cfr_wide(T, N.first_edge)[a];
+      CfrWide& W = cfr_wide(T, fe)[a];
       const double* wp = cfr_node(T, E[a].child).wp;
       double w[6];
       for (int p = 0; p < 6; p++) w[p] = wp[p];
@@ -1134,8 +1216,8 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
     return;
   }
 #endif
-  if (!(N.flags & NF_ROLE_PICK)) {
-    int p = N.player;
+  if (!(flags & NF_ROLE_PICK)) {
+    int p = player;
     double mx = cfr_node(T, E[0].child).wp[p];
     for (int a = 1; a < nch; a++) {
       double v = cfr_node(T, E[a].child).wp[p];
@@ -1143,7 +1225,7 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n) {
     }
     for (int a = 0; a < nch; a++) E[a].R += mx - cfr_node(T, E[a].child).wp[p];
   } else {
-    CfrWide* W = cfr_wide(T, N.first_edge);
+    CfrWide* W = cfr_wide(T, fe);
     for (int a = 0; a < nch; a++) {
       const double* wp = cfr_node(T, E[a].child).wp;
       double mx = wp[0];
@@ -1169,7 +1251,7 @@ CIT_NOINLINE void cfr_backprop(CfrTree& T_in, int n, double r0, double r1, doubl
     double s = 0.0;
     for (int k = 0; k < 6; k++) s += N.nv[k];
     for (int k = 0; k < 6; k++) N.wp[k] = N.nv[k] / s;
-    if (N.n_children) cfr_update_regrets(T, n);
+    if (N.n_children) cfr_update_regrets(T, n, N.n_children, N.first_edge, N.flags, N.player);
     n = N.parent;
   }
 }
@@ -1178,6 +1260,11 @@ CIT_HD void cfr_backprop_arr(CfrTree& T, int n, const double* rw, bool model) {
 }
 
 // ---------------------------------------------------------------- drivers
+// first_edge of node n: the cached current node's without a read.
+CIT_HD int cfr_first_edge(const CfrTree& T, int n) {
+  return cfr_u(T.cur_node) == n ? cfr_u(T.cur_fe) : cfr_node(T, n).first_edge;
+}
+
 // cfr_train(iters) (:187-205) on the game in working row 0 (the root's game:
 // skip_false_choice mutates it, as the reference mutates the game passed to
 // CFRNode), as resumable slices (the tree queue of simulate_games): phase
@@ -1228,7 +1315,7 @@ CIT_HD int cfr_train_slice(CfrTree& T_in, CfrState& S_in, int iters, bool root_s
     cfr_update_strategy(T, n);
     int a = cfr_u(cfr_choose(T, n));
     if (T.err) break;
-    n = (*cfr_edge(T, cfr_node(T, n).first_edge + a)).child;
+    n = (*cfr_edge(T, cfr_first_edge(T, n) + a)).child;
     if (cfr_node(T, n).flags & NF_TERMINAL) {
       double rw[6] = {0, 0, 0, 0, 0, 0};
       if (cfr_node(T, n).winner >= 0) rw[cfr_node(T, n).winner] = 1.0;
@@ -1365,7 +1452,7 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
     cfr_update_strategy(T, S.cur);
     int a = cfr_u(cfr_choose(T, S.cur));
     if (T.err) break;
-    int n = (*cfr_edge(T, cfr_node(T, S.cur).first_edge + a)).child;
+    int n = (*cfr_edge(T, cfr_first_edge(T, S.cur) + a)).child;
     CfrNode& N = cfr_node(T, n);
     if (N.depth > max_depth && !(N.flags & NF_TERMINAL)) {
       cfr_expand(T, n);

@@ -21,6 +21,7 @@ do not depend on the world size) and runs them as one batch on its GPU:
 All device work goes through libcitadels_hip.so (engine.GameBatch); nothing
 here falls back to the CPU.
 """
+import json
 import os
 import time
 
@@ -329,6 +330,10 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     n_requeued = 0
     # CIT_QUEUE_PROF=1: wall time per phase (synchronising after each; diagnosis only)
     qprof = {"plan": 0.0, "slice+targets": 0.0, "finish": 0.0} if os.environ.get("CIT_QUEUE_PROF") else None
+    # CIT_QUEUE_TRACE=path: one JSON line per slice (time, live / paused / searching trees, trees done,
+    # arena blocks held) -- where the queue's time goes (diagnosis only)
+    qtrace = open(os.environ["CIT_QUEUE_TRACE"], "w") if os.environ.get("CIT_QUEUE_TRACE") else None
+    t_q0 = time.perf_counter()
 
     def tick(key, t0):
         if qprof is None:
@@ -432,11 +437,20 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
                 slot_q[fs[:k]] = new_q
             slot_q[fs[k:]] = -1
         tq = tick("finish", tq)
+        if qtrace is not None:
+            held = planner.held().sum(0).tolist() if planner is not None else None
+            qtrace.write(json.dumps({"slice": n_slices, "t": round(time.perf_counter() - t_q0, 4),
+                                     "slots_busy": int((slot_q >= 0).sum()), "searching": int(ran.sum()),
+                                     "paused": 0 if paused is None else int(paused.numel()), "done": n_done,
+                                     "held_blocks": held, "arena_blocks": None if planner is None
+                                     else planner.cap.tolist()}) + "\n")
         if int(running.item()) == 0 and pending is None and bool((slot_q < 0).all()) and not requeue:
             break
     if log is not None and planner is not None:
         log("simulate_queue: %d slots (overcommit %.2f), %d tree-slices paused, %d trees restarted after the "
             "arena ran out" % (S, overcommit, planner.paused_slices, n_requeued))
+    if qtrace is not None:
+        qtrace.close()
     if log is not None and qprof is not None:
         log("simulate_queue phases (s): %s over %d slices" % ({k: round(v, 2) for k, v in qprof.items()}, n_slices))
     sb.pool = None

@@ -196,6 +196,53 @@ def test_gpu_rollout_streams_overlap(engine):
         assert np.array_equal(gb.winner.cpu().numpy(), alone[k][2]), k
 
 
+def test_gpu_continuous_loop_with_init(engine):
+    """bench.py's e2e loop: K batches re-initialised (cit_init = the LDS-free
+    k_mt_seed_cpython + k_init) and rolled out, init + rollout of batch k on
+    stream k % 3, so inits run beside earlier batches' rollouts.  Every batch
+    equals the same batch initialised and rolled out alone (rows, steps,
+    winners, both stream words and positions), and a batch seeded by the
+    one-game-per-lane restatement of random.seed (cit_mt_seed, cit_core.h's
+    mt_seed_cpython) and dealt by k_init from that stream equals cit_init's."""
+    from citadels_self_play_amd import _lib
+    lib = _lib.load()
+    B, K, S = 4096, 6, 3
+    seeds = [np.arange(11_000_000 + k * B, 11_000_000 + (k + 1) * B) for k in range(K)]
+    alone = []
+    for s in seeds:
+        a = engine(s, preset=True)
+        init_rows, init_mt = a.rows(), a.mt.cpu().numpy().copy()
+        st, w = a.rollout(games_per_block=0)
+        torch.cuda.synchronize()
+        alone.append((init_rows, init_mt, a.rows(), st.cpu().numpy().copy(), w.cpu().numpy().copy(),
+                      a.mt.cpu().numpy().copy(), a.mt_idx.cpu().numpy().copy()))
+    # the seeding restated one game per lane, then the deal from that stream
+    b = engine(seeds[0], preset=True)
+    sd = torch.as_tensor(seeds[0], dtype=torch.int64, device="cuda")
+    b.games.zero_()
+    _lib.check(lib.cit_mt_seed(b.mt.data_ptr(), b.mt_idx.data_ptr(), B, sd.data_ptr(), 0, _stream()), "seed")
+    _lib.check(lib.cit_init(b.games.data_ptr(), b.mt.data_ptr(), b.mt_idx.data_ptr(), B, None, 1, _stream()), "init")
+    torch.cuda.synchronize()
+    assert np.array_equal(b.rows(), alone[0][0])
+    batches = [engine(s, preset=True) for s in seeds]
+    for gb in batches:                                  # played-out games, as in the bench before e2e
+        gb.rollout(games_per_block=0)
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    torch.cuda.synchronize()
+    for k, gb in enumerate(batches):
+        with torch.cuda.stream(streams[k % S]):
+            gb.reset()
+            gb.rollout(games_per_block=0)
+    torch.cuda.synchronize()
+    for k, gb in enumerate(batches):
+        _, _, rows, st, w, mt, idx = alone[k]
+        assert int((gb.errors() != 0).sum()) == 0, k
+        assert np.array_equal(gb.rows(), rows), k
+        assert np.array_equal(gb.steps.cpu().numpy(), st), k
+        assert np.array_equal(gb.winner.cpu().numpy(), w), k
+        assert np.array_equal(gb.mt.cpu().numpy(), mt) and np.array_equal(gb.mt_idx.cpu().numpy(), idx), k
+
+
 def test_gpu_rollout_u_option_overflow(engine):
     """Random-role games (thousands of options per step for the cardinal /
     magician) through k_rollout_u at B = 1024: a draw k >= 64 misses the LDS

@@ -492,7 +492,32 @@ CIT_HD void row_load(const CfrTree& T, uint32_t* dst, int id) {
   const uint32_t* base = cfr_base(T);
   CFR_SYNC();
 #if CIT_WAVE
-  {   // lanes 0..12 hold the mask words; chunk j = dwords 64j..64j+63 on the 64 lanes
+  if (cfr_u(T.row_cap) + CFR_ROW_HDR <= 4 * 64) {
+    // the whole slot in one round of loads (up to 4 dwords per lane, more than
+    // the differing dwords need: latency, not bytes, bounds the search), staged
+    // in the LDS scratch so each lane can read its dwords' values by rank;
+    // lanes 0..12 hold the mask words, chunk j = dwords 64j..64j+63
+    const int l = CFR_LANE, nw = cfr_u(T.row_cap) + CFR_ROW_HDR;
+    uint32_t* stg = reinterpret_cast<uint32_t*>(cfr_ls.tmp);
+    static_assert(4 * 64 * 4 <= CIT_SAMPLE_SCRATCH, "row staging fits the scratch");
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = l + 64 * k < nw ? s[l + 64 * k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (l + 64 * k < nw) stg[l + 64 * k] = v[k];
+    const uint32_t mw = v[0];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < (CFR_ROW_W + 63) / 64; j++) {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mw, 2 * j);
+      const uint32_t hi = 2 * j + 1 < CFR_ROW_MASKW ? (uint32_t)__builtin_amdgcn_readlane((int)mw, 2 * j + 1) : 0u;
+      const uint64_t m = ((uint64_t)hi << 32) | lo;
+      const int d = 64 * j + l;
+      if (d < CFR_ROW_W) dst[d] = ((m >> l) & 1) ? stg[CFR_ROW_HDR + acc + cfr_mbcnt(m)] : base[d];
+      acc += (uint32_t)__popcll(m);
+    }
+  } else {   // lanes 0..12 hold the mask words; chunk j = dwords 64j..64j+63 on the 64 lanes
     const int l = CFR_LANE;
     const uint32_t mw = l < CFR_ROW_MASKW ? s[l] : 0u;
     uint32_t acc = 0;
@@ -1057,13 +1082,16 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
     const int l = CFR_LANE;
     const bool h0 = l < nch, h1 = l + 64 < nch;
     double r0 = 0.0, c0 = 0.0, r1 = 0.0, c1 = 0.0;
+    int k0 = -1, k1 = -1;
     if (h0) {
       r0 = E[l].R;
       c0 = E[l].CS;
+      k0 = E[l].child;
     }
     if (h1) {
       r1 = E[l + 64].R;
       c1 = E[l + 64].CS;
+      k1 = E[l + 64].child;
     }
     if (h0) sb[l] = exp((-r0) * CFR_LN13);
     if (h1) sb[l + 64] = exp((-r1) * CFR_LN13);
@@ -1092,6 +1120,11 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
       E[l + 64].CS = v;
       cb[l + 64] = v;
     }
+    // the children's ids, loaded with R and CS, kept in the spent S copies for
+    // the step to the chosen child (cfr_child)
+    int* kids = reinterpret_cast<int*>(sb);
+    if (h0) kids[l] = k0;
+    if (h1) kids[l + 64] = k1;
     CFR_SYNC();
     cfr_ls.cnode = n;
     cfr_ls.cnch = nch;
@@ -1264,6 +1297,15 @@ CIT_HD void cfr_backprop_arr(CfrTree& T, int n, const double* rw, bool model) {
 CIT_HD int cfr_first_edge(const CfrTree& T, int n) {
   return cfr_u(T.cur_node) == n ? cfr_u(T.cur_fe) : cfr_node(T, n).first_edge;
 }
+// Child a of node n: from the ids cfr_update_strategy(n) loaded with the
+// regrets (device LDS path), else from the edge record.
+CIT_HD int cfr_child(const CfrTree& T, int n, int a) {
+#if CIT_WAVE
+  if (cfr_u(cfr_ls.cnode) == n && cfr_u(T.cur_node) == n)
+    return cfr_u(reinterpret_cast<const int*>(cfr_ls.sbuf)[a]);
+#endif
+  return (*cfr_edge(T, cfr_first_edge(T, n) + a)).child;
+}
 
 // cfr_train(iters) (:187-205) on the game in working row 0 (the root's game:
 // skip_false_choice mutates it, as the reference mutates the game passed to
@@ -1315,7 +1357,7 @@ CIT_HD int cfr_train_slice(CfrTree& T_in, CfrState& S_in, int iters, bool root_s
     cfr_update_strategy(T, n);
     int a = cfr_u(cfr_choose(T, n));
     if (T.err) break;
-    n = (*cfr_edge(T, cfr_first_edge(T, n) + a)).child;
+    n = cfr_u(cfr_child(T, n, a));
     if (cfr_node(T, n).flags & NF_TERMINAL) {
       double rw[6] = {0, 0, 0, 0, 0, 0};
       if (cfr_node(T, n).winner >= 0) rw[cfr_node(T, n).winner] = 1.0;
@@ -1452,7 +1494,7 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
     cfr_update_strategy(T, S.cur);
     int a = cfr_u(cfr_choose(T, S.cur));
     if (T.err) break;
-    int n = (*cfr_edge(T, cfr_first_edge(T, S.cur) + a)).child;
+    int n = cfr_u(cfr_child(T, S.cur, a));
     CfrNode& N = cfr_node(T, n);
     if (N.depth > max_depth && !(N.flags & NF_TERMINAL)) {
       cfr_expand(T, n);

@@ -70,7 +70,10 @@ __device__ __forceinline__ uint64_t cit_wave_or64(uint64_t v) {
 #define CIT_KH_MAX 32
 #define CIT_KH_POOL 244          // cards held by HandKnowledge entries (88 at most in 1,920 cfr_train(200000) trees)
 #define CIT_SEVEN_CAP 8
-#define CIT_HAND_MASK_MAX 60      // magician / cardinal hand-slot masks (uint64_t) and binom() range
+// magician / cardinal options over hands of at most this many cards (their
+// hand-slot masks and slot tables); the reference lists every combination of
+// the hand there (itertools: 2^33 tuples at 33 cards), a search it cannot run
+#define CIT_HAND_MASK_MAX 32
 
 // ------------------------------------------------------------------- errors
 // A lane whose reference run would raise (or that overflows a fixed capacity)

@@ -166,15 +166,14 @@ CIT_HD void area_splice(CitGame& g, CitPlayer& P, int L, int at, int del, int in
     if (l + 64 < ins) P.hand[cut + l + 64] = (uint8_t)s1;
   }
 #else
-  {
-    uint8_t tmp[CIT_AREA_CAP];
-    for (int i = 0; i < ins; i++) tmp[i] = (uint8_t)src(i);
+  {   // serial: the lists after the cut move first, then src fills the gap (src must
+      // not read the area here -- no serial caller's does -- so no private copy is needed)
     const int shift = ins - del, from = cut + del, tail = used - from;
     if (shift > 0)
       for (int i = tail - 1; i >= 0; i--) P.hand[from + i + shift] = P.hand[from + i];
     else if (shift < 0)
       for (int i = 0; i < tail; i++) P.hand[from + i + shift] = P.hand[from + i];
-    for (int i = 0; i < ins; i++) P.hand[cut + i] = tmp[i];
+    for (int i = 0; i < ins; i++) P.hand[cut + i] = (uint8_t)src(i);
   }
 #endif
   area_set_len(P, L, area_len(P, L) - del + ins);
@@ -1132,9 +1131,7 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
       return false;
     case R_MAGICIAN: {
       int n = P.n_hand;
-      // hand-slot masks are 64-bit and binom() exact to n = 60; the reference
-      // lists all 2^n - 1 combinations here (itertools), ~1e18 at n = 60
-      if (n > CIT_HAND_MASK_MAX) { s.err |= CIT_ERR_UNSUPPORTED; return true; }
+      if (n > CIT_HAND_MASK_MAX) { s.err |= CIT_ERR_UNSUPPORTED; return true; }   // (cit_core.h)
       for (int p = 0; p < CIT_NP; p++)
         if (p != a) EMIT(mk(O_MAGIC_HAND_CHANGE, a, p));
       for (int r = 1; r <= n; r++) {
@@ -1539,7 +1536,11 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
 //    which consume the game's CPython stream inside get_options; the drawn
 //    permutations go to `seer` (CIT_SEER_MAX packed options per lane:
 //    card i in byte i, handout count in byte 7).
-#define CIT_SEER_MAX (5 * CIT_AREA_CAP * 3)
+// (+ CIT_AREA_CAP bytes after the options: the shuffled `rest` list of the
+// give-back draws, kept out of private memory)
+#define CIT_SEER_OPTS (5 * CIT_AREA_CAP * 3)
+#define CIT_SEER_MAX (CIT_SEER_OPTS + CIT_AREA_CAP / 8)
+static_assert(CIT_AREA_CAP % 8 == 0, "seer scratch tail in whole words");
 CIT_HD void cit_prepare_options(CitGame& g, CitMT& rng, uint64_t* seer) {
   g.n_sch = 0;
   if ((g.gs_state != 9 && g.gs_state != 8) || g.gs_pid < 0) return;
@@ -1550,10 +1551,10 @@ CIT_HD void cit_prepare_options(CitGame& g, CitMT& rng, uint64_t* seer) {
     if (!seer) return;         // the enumerator reports UNSUPPORTED
     int k = g.n_seer == 255 ? 0 : g.n_seer;
     int n = P.n_hand, o = 0;
+    uint8_t* rest = reinterpret_cast<uint8_t*>(seer + CIT_SEER_OPTS);
     for (int pos = 0; pos < k; pos++) {
       for (int j = 0; j < n; j++) {
         int card = P.hand[j], t = card_type(card);
-        uint8_t rest[CIT_AREA_CAP];
         int m = 0;
         for (int q = 0; q < n; q++)
           if (card_type(P.hand[q]) != t) rest[m++] = P.hand[q];
@@ -1933,12 +1934,21 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
         area_splice(g, T, AL_HAND, 0, nt, np, [p0, p1](int i) { return i < 64 ? p0 : p1; });
       }
 #else
-      {
-        uint8_t hp[CIT_AREA_CAP], ht[CIT_AREA_CAP];
-        for (int i = 0; i < np; i++) hp[i] = P.hand[i];
-        for (int i = 0; i < nt; i++) ht[i] = T.hand[i];
-        area_splice(g, P, AL_HAND, 0, np, nt, [&ht](int i) { return ht[i]; });
-        area_splice(g, T, AL_HAND, 0, nt, np, [&hp](int i) { return hp[i]; });
+      {   // swap the common prefix in place, then move the longer hand's rest over
+          // one card at a time (no private copy of a hand)
+        const int m = np < nt ? np : nt;
+        for (int i = 0; i < m; i++) {
+          uint8_t c = P.hand[i];
+          P.hand[i] = T.hand[i];
+          T.hand[i] = c;
+        }
+        CitPlayer& A = np < nt ? P : T;     // receives the extra cards
+        CitPlayer& Z = np < nt ? T : P;
+        for (int i = m; i < (np < nt ? nt : np); i++) {
+          const int c = Z.hand[m];
+          area_splice(g, Z, AL_HAND, m, 1, 0, [](int) { return 0; });
+          pl_put(g, A, AL_HAND, c);
+        }
       }
 #endif
       at5(g, a, ADM_ABILITY);

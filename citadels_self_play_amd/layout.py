@@ -12,7 +12,7 @@ DECK_CAP, DISCARD_CAP, USED_CAP = 128, 88, 80
 KH_MAX, KH_POOL, SEVEN_CAP = 32, 244, 8
 GAME_BYTES = 1552
 MT_N = 624
-SEER_MAX = 5 * AREA_CAP * 3      # CIT_SEER_MAX: packed seer give-back options per lane
+SEER_MAX = 5 * AREA_CAP * 3 + AREA_CAP // 8   # CIT_SEER_MAX: seer give-back options (+ their shuffle list) per lane
 NO_CARD = 255
 ROLE_BEWITCHED, ROLE_NONE = 27, 255
 

@@ -44,6 +44,8 @@ _SIGS = {
     "cit_cfr_arena_reset": ([vp, i32, i32, i32, i32, i32, vp], i32),
     "cit_cfr_arena_bytes_rows": ([i32, i32, i32], i64),
     "cit_cfr_arena_reset_rows": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
+    "cit_cfr_arena_bytes_fmt": ([i32, i32, i32, i32], i64),
+    "cit_cfr_arena_reset_fmt": ([vp, i32, i32, i32, i32, i32, i32, i32, vp], i32),
     "cit_cfr_arena_release": ([vp, i32, i32, i32, vp, i32, vp], i32),
     "cit_cfr_train_slice": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, i64, vp, vp, vp, vp], i32),
     "cit_count_options": ([vp, vp, vp, vp, i32, vp, vp], i32),

@@ -42,9 +42,15 @@
 #define CFR_LN13 0x1.0ca937be1b9dcp-2   // np.log(1.3)
 #define CFR_ATOL 1.4901161193847656e-08  // sqrt(finfo(float64).eps), numpy choice's p check
 
-enum { NF_ROLE_PICK = 1, NF_TERMINAL = 2, NF_PRED = 4 };
+// NF_BACKED: backpropagate has run on the node (winning_probabilities is then
+// node_value / node_value.sum(), else its initial zeros)
+enum { NF_ROLE_PICK = 1, NF_TERMINAL = 2, NF_PRED = 4, NF_BACKED = 8 };
 
-struct CfrNode {                       // 168 B
+// A node record: the header and node_value.  winning_probabilities is derived
+// (cfr_wp: backpropagate sets it to node_value / node_value.sum() whenever it
+// touches node_value); pred_node_value lives in a side array that only pools
+// of cfr_pred searches have (cfr_pred_of).  72 B instead of round 3's 168.
+struct CfrNode {                       // 72 B
   int32_t parent, first_edge;
   int16_t n_children, edge_cap, depth;
   int8_t player, gs_state;
@@ -52,8 +58,17 @@ struct CfrNode {                       // 168 B
   int8_t winner;
   int16_t sib;                         // index among the parent's children (-1: root)
   uint8_t pad[4];
-  double nv[6], wp[6], pred[6];
+  double nv[6];
 };
+#define CFR_PRED_BYTES 48              // pred_node_value f64[6] per node (cfr_pred pools)
+// node_value.sum() in numpy's order (pairwise_sum below 8 elements: sequential)
+CIT_HD double cfr_nv_sum(const double* nv) {
+  double s = 0.0;
+  for (int k = 0; k < 6; k++) s += nv[k];
+  return s;
+}
+// winning_probabilities[p] of a node with node_value nv, flags f (s = cfr_nv_sum(nv))
+CIT_HD double cfr_wp(const double* nv, double s, int f, int p) { return (f & NF_BACKED) ? nv[p] / s : 0.0; }
 // An edge = (option, child) and the parent's regret / strategy / cumulative
 // strategy entries for it.  A normal node's arrays are [nch] (one double per
 // edge).  A role-pick node's are [6 players, 10]: it reserves
@@ -68,7 +83,7 @@ struct CfrEdge {                       // 48 B
 struct CfrWide {                       // 144 B = 3 edge slots
   double R[6], S[6], CS[6];
 };
-static_assert(sizeof(CfrNode) == 168, "CfrNode layout");
+static_assert(sizeof(CfrNode) == 72, "CfrNode layout");
 static_assert(sizeof(CfrEdge) == 48, "CfrEdge layout");
 static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
 #define CFR_ROLE_EDGE_SLOTS (CFR_ROLE_CHILDREN * 4)   // 10 edges + 10 wide records
@@ -108,7 +123,8 @@ struct CfrArena {                             // 64 B, written by cit_cfr_arena_
   uint32_t n_next, n_cap, e_next, e_cap;      // never-used blocks handed out / capacity
   uint32_t n_head, n_tail, e_head, e_tail;    // free rings: taken / released counts (mod cap)
   uint32_t row_cap;                           // row slot format (0: raw rows)
-  uint32_t pad[7];
+  uint32_t pred;                              // 1: node blocks carry pred_node_value (cfr_pred pools)
+  uint32_t pad[6];
 };
 #define CFR_ROW_W (CIT_GAME_BYTES / 4)        // 388 dwords
 #define CFR_ROW_HDR 16                        // header words of a diff row slot
@@ -118,6 +134,7 @@ static_assert(sizeof(CfrArena) == 64, "CfrArena layout");
 
 struct CfrTree {
   uint8_t* node_base;                  // arena node records
+  uint8_t* pred_base;                  // arena pred_node_value arrays (pools with pred)
   uint8_t* row_base;                   // arena node rows
   uint8_t* edge_base;                  // arena edges
   CfrArena* arena;
@@ -163,13 +180,13 @@ CIT_HD int cfr_row_cap_ok(int row_cap) { return row_cap == 0 || (row_cap > 0 && 
 CIT_HD int64_t cfr_row_slot_bytes(int row_cap) {
   return row_cap > 0 ? (int64_t)4 * (CFR_ROW_HDR + row_cap) : (int64_t)CIT_GAME_BYTES;
 }
-CIT_HD int64_t cfr_node_block_bytes(int row_cap = 0) {
-  return (int64_t)CFR_NB * ((int64_t)sizeof(CfrNode) + cfr_row_slot_bytes(row_cap));
+CIT_HD int64_t cfr_node_block_bytes(int row_cap = 0, int pred = 1) {
+  return (int64_t)CFR_NB * ((int64_t)sizeof(CfrNode) + (pred ? CFR_PRED_BYTES : 0) + cfr_row_slot_bytes(row_cap));
 }
 CIT_HD int64_t cfr_ring_bytes(int64_t n_blocks, int64_t e_blocks) { return (4 * (n_blocks + e_blocks) + 15) & ~(int64_t)15; }
-CIT_HD int64_t cfr_arena_bytes(int n_blocks, int e_blocks, int row_cap = 0) {
+CIT_HD int64_t cfr_arena_bytes(int n_blocks, int e_blocks, int row_cap = 0, int pred = 1) {
   return (int64_t)sizeof(CfrArena) + cfr_ring_bytes(n_blocks, e_blocks) +
-         (int64_t)n_blocks * cfr_node_block_bytes(row_cap) + (int64_t)e_blocks * CFR_EB * (int64_t)sizeof(CfrEdge);
+         (int64_t)n_blocks * cfr_node_block_bytes(row_cap, pred) + (int64_t)e_blocks * CFR_EB * (int64_t)sizeof(CfrEdge);
 }
 // Binds tree l of a B-tree pool; the arena's capacities come from its header.
 CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, int B, long l, int node_cap, int edge_cap) {
@@ -187,7 +204,8 @@ CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, int B, long l, int node_cap
   T.row_cap = (int)T.arena->row_cap;
   T.row_slot = cfr_row_slot_bytes(T.row_cap);
   T.node_base = a + sizeof(CfrArena) + cfr_ring_bytes(ncap, ecap);
-  T.row_base = T.node_base + ncap * CFR_NB * (int64_t)sizeof(CfrNode);
+  T.pred_base = T.node_base + ncap * CFR_NB * (int64_t)sizeof(CfrNode);
+  T.row_base = T.pred_base + (T.arena->pred ? ncap * CFR_NB * (int64_t)CFR_PRED_BYTES : 0);
   T.edge_base = T.row_base + ncap * CFR_NB * T.row_slot;
   T.node_cap = node_cap;
   T.edge_cap = edge_cap;
@@ -368,6 +386,10 @@ CIT_HD int64_t cfr_node_slot(const CfrTree& T, int n) {
 }
 CIT_HD CfrNode& cfr_node(const CfrTree& T, int n) {
   return *reinterpret_cast<CfrNode*>(cfr_glb(T.node_base) + cfr_node_slot(T, n) * (int64_t)sizeof(CfrNode));
+}
+// node n's pred_node_value (pools with pred only)
+CIT_HD double* cfr_pred_of(const CfrTree& T, int n) {
+  return reinterpret_cast<double*>(cfr_glb(T.pred_base) + cfr_node_slot(T, n) * (int64_t)CFR_PRED_BYTES);
 }
 CIT_HD CfrEdge* cfr_edge(const CfrTree& T, int e) {
   int64_t slot = (int64_t)cfr_ebt_at(T, e >> CFR_EB_SHIFT) * CFR_EB + (e & (CFR_EB - 1));
@@ -844,7 +866,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   T.n_nodes = id + 1;
   CfrNode& N = cfr_node(T, id);
 #if CIT_WAVE
-  {   // the header's 6 words and the 36 zero words of nv / wp / pred, one store per lane
+  {   // the header's 6 words and the 12 zero words of nv, one store per lane
     uint32_t hw[6];
     hw[0] = (uint32_t)parent;
     hw[1] = (uint32_t)-1;
@@ -869,7 +891,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   N.flags = (uint8_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0));
   N.winner = w.winner;
   N.sib = -1;
-  for (int k = 0; k < 6; k++) N.nv[k] = N.wp[k] = N.pred[k] = 0.0;
+  for (int k = 0; k < 6; k++) N.nv[k] = 0.0;
 #endif
   if (id == 0) row_set_base(T, w_row(T, which));   // the root: the tree's base row
   row_store(T, id, w_row(T, which));
@@ -1230,7 +1252,11 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n, int nch, int fe, int 
     const int a = CFR_LANE;
     if (!(flags & NF_ROLE_PICK)) {
       int p = player;
-      double v = a < nch ? cfr_node(T, E[a].child).wp[p] : 0.0;
+      double v = 0.0;
+      if (a < nch) {
+        const CfrNode& C = cfr_node(T, E[a].child);
+        v = cfr_wp(C.nv, cfr_nv_sum(C.nv), C.flags, p);
+      }
       double mx = cfr_readlane_f64(v, 0);
       for (int k = 1; k < nch; k++) {
         double x = cfr_readlane_f64(v, k);
@@ -1239,9 +1265,11 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n, int nch, int fe, int 
       if (a < nch) E[a].R += mx - v;
     } else if (a < nch) {
       CfrWide& W = cfr_wide(T, fe)[a];
-      const double* wp = cfr_node(T, E[a].child).wp;
+      const CfrNode& C = cfr_node(T, E[a].child);
+      const double cs = cfr_nv_sum(C.nv);
+      const int cf = C.flags;
       double w[6];
-      for (int p = 0; p < 6; p++) w[p] = wp[p];
+      for (int p = 0; p < 6; p++) w[p] = cfr_wp(C.nv, cs, cf, p);
       double mx = w[0];
       for (int p = 1; p < 6; p++) mx = (mx != mx || w[p] != w[p]) ? NAN : (w[p] > mx ? w[p] : mx);
       for (int p = 0; p < 6; p++) W.R[p] += mx - w[p];
@@ -1249,18 +1277,23 @@ CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n, int nch, int fe, int 
     return;
   }
 #endif
+  auto wp_of = [&T](int c, int p) {
+    const CfrNode& C = cfr_node(T, c);
+    return cfr_wp(C.nv, cfr_nv_sum(C.nv), C.flags, p);
+  };
   if (!(flags & NF_ROLE_PICK)) {
     int p = player;
-    double mx = cfr_node(T, E[0].child).wp[p];
+    double mx = wp_of(E[0].child, p);
     for (int a = 1; a < nch; a++) {
-      double v = cfr_node(T, E[a].child).wp[p];
+      double v = wp_of(E[a].child, p);
       if (v > mx) mx = v;
     }
-    for (int a = 0; a < nch; a++) E[a].R += mx - cfr_node(T, E[a].child).wp[p];
+    for (int a = 0; a < nch; a++) E[a].R += mx - wp_of(E[a].child, p);
   } else {
     CfrWide* W = cfr_wide(T, fe);
     for (int a = 0; a < nch; a++) {
-      const double* wp = cfr_node(T, E[a].child).wp;
+      double wp[6];
+      for (int p = 0; p < 6; p++) wp[p] = wp_of(E[a].child, p);
       double mx = wp[0];
       for (int p = 1; p < 6; p++) mx = (mx != mx || wp[p] != wp[p]) ? NAN : (wp[p] > mx ? wp[p] : mx);
       for (int p = 0; p < 6; p++) W[a].R[p] += mx - wp[p];
@@ -1277,13 +1310,10 @@ CIT_NOINLINE void cfr_backprop(CfrTree& T_in, int n, double r0, double r1, doubl
   const double reward[6] = {r0, r1, r2, r3, r4, r5};
   while (n >= 0) {
     CfrNode& N = cfr_node(T, n);
-    double s0 = 0.0;
-    for (int k = 0; k < 6; k++) s0 += N.nv[k];
+    double s0 = cfr_nv_sum(N.nv);
     if (T.training || s0 == 0.0 || !model)
       for (int k = 0; k < 6; k++) N.nv[k] += reward[k];
-    double s = 0.0;
-    for (int k = 0; k < 6; k++) s += N.nv[k];
-    for (int k = 0; k < 6; k++) N.wp[k] = N.nv[k] / s;
+    if (!(N.flags & NF_BACKED)) N.flags |= NF_BACKED;     // winning_probabilities = nv / nv.sum() from now on
     if (N.n_children) cfr_update_regrets(T, n, N.n_children, N.first_edge, N.flags, N.player);
     n = N.parent;
   }
@@ -1480,9 +1510,10 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
   } else if (S.phase == CP_WAIT) {
     int n = S.pending;
     CfrNode& N = cfr_node(T, n);
-    for (int k = 0; k < 6; k++) N.pred[k] = (double)(5.0f * probs[k]);   // model_reward_weights * wp (float32)
+    double* pred = cfr_pred_of(T, n);
+    for (int k = 0; k < 6; k++) pred[k] = (double)(5.0f * probs[k]);   // model_reward_weights * wp (float32)
     N.flags |= NF_PRED;
-    cfr_backprop_arr(T, n, N.pred, true);
+    cfr_backprop_arr(T, n, pred, true);
     cfr_update_strategy(T, n);
     S.cur = S.root;
     S.it++;
@@ -1505,7 +1536,7 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
         S.phase = CP_WAIT;
         return 1;
       }
-      cfr_backprop_arr(T, n, cfr_node(T, n).pred, true);
+      cfr_backprop_arr(T, n, cfr_pred_of(T, n), true);
       cfr_update_strategy(T, n);
       S.cur = S.root;
     } else if (N.flags & NF_TERMINAL) {

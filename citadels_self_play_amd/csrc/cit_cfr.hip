@@ -315,12 +315,12 @@ __global__ void k_arena_release(int32_t* tables, long per_words, int nb, int eb,
 // Only the tables of each tree's region are set (its base / scratch rows are
 // written before they are read).
 __global__ void k_arena_reset(int32_t* pool, long per_words, long tbl_words, int B, CfrArena* a, uint32_t n_cap,
-                              uint32_t e_cap, uint32_t row_cap) {
+                              uint32_t e_cap, uint32_t row_cap, uint32_t pred) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < tbl_words * B) pool[(i / tbl_words) * per_words + i % tbl_words] = -1;
   if (blockIdx.x == 0 && threadIdx.x < sizeof(CfrArena) / 4)
-    reinterpret_cast<uint32_t*>(a)[threadIdx.x] =
-        threadIdx.x == 1 ? n_cap : threadIdx.x == 3 ? e_cap : threadIdx.x == 8 ? row_cap : 0u;
+    reinterpret_cast<uint32_t*>(a)[threadIdx.x] = threadIdx.x == 1 ? n_cap : threadIdx.x == 3 ? e_cap
+                                                 : threadIdx.x == 8 ? row_cap : threadIdx.x == 9 ? pred : 0u;
 }
 
 // Row slot format of each pool this library reset (cit_cfr_arena_reset_rows),
@@ -357,6 +357,9 @@ DynLds dyn_lds(const void* pool, int node_cap, int edge_cap) {
 
 extern "C" {
 
+int cit_cfr_arena_reset_fmt(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                            int row_cap, int pred, hipStream_t stream);
+
 int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap) {
   if (node_cap <= 0 || edge_cap <= 0 || cfr_nblocks(node_cap) > CFR_TBL_MAX || cfr_eblocks(edge_cap) > CFR_TBL_MAX)
     return -1;
@@ -370,6 +373,10 @@ int64_t cit_cfr_arena_bytes_rows(int node_blocks, int edge_blocks, int row_cap) 
   if (node_blocks < 0 || edge_blocks < 0 || !cfr_row_cap_ok(row_cap)) return -1;
   return cfr_arena_bytes(node_blocks, edge_blocks, row_cap);
 }
+int64_t cit_cfr_arena_bytes_fmt(int node_blocks, int edge_blocks, int row_cap, int pred) {
+  if (node_blocks < 0 || edge_blocks < 0 || !cfr_row_cap_ok(row_cap)) return -1;
+  return cfr_arena_bytes(node_blocks, edge_blocks, row_cap, pred != 0);
+}
 int cit_cfr_block_sizes(int32_t* out) {
   if (!out) return -1;
   out[0] = CFR_NB;
@@ -379,6 +386,10 @@ int cit_cfr_block_sizes(int32_t* out) {
 }
 int cit_cfr_arena_reset_rows(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
                              int row_cap, hipStream_t stream) {
+  return cit_cfr_arena_reset_fmt(pool, B, node_cap, edge_cap, node_blocks, edge_blocks, row_cap, 1, stream);
+}
+int cit_cfr_arena_reset_fmt(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                            int row_cap, int pred, hipStream_t stream) {
   if (!pool || B <= 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || node_blocks < 0 || edge_blocks < 0 ||
       !cfr_row_cap_ok(row_cap))
     return -1;
@@ -389,7 +400,7 @@ int cit_cfr_arena_reset_rows(void* pool, int B, int node_cap, int edge_cap, int 
   long n = tbl_words * B;
   hipLaunchKernelGGL(k_arena_reset, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (int32_t*)pool,
                      per_words, tbl_words, B, reinterpret_cast<CfrArena*>(a), (uint32_t)node_blocks,
-                     (uint32_t)edge_blocks, (uint32_t)row_cap);
+                     (uint32_t)edge_blocks, (uint32_t)row_cap, (uint32_t)(pred != 0));
   CHECK_LAUNCH();
 }
 int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,

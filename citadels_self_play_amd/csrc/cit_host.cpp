@@ -167,8 +167,8 @@ int64_t cith_cfr_arena_bytes(int node_blocks, int edge_blocks) { return cfr_aren
 int64_t cith_cfr_arena_bytes_rows(int node_blocks, int edge_blocks, int row_cap) {
   return cfr_row_cap_ok(row_cap) ? cfr_arena_bytes(node_blocks, edge_blocks, row_cap) : -1;
 }
-void cith_cfr_arena_reset_rows(uint8_t* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
-                               int row_cap) {
+void cith_cfr_arena_reset_fmt(uint8_t* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                              int row_cap, int pred) {
   int64_t tb = cfr_pool_bytes(node_cap, edge_cap) * (int64_t)B;
   memset(pool, 0xff, (size_t)tb);
   CfrArena* a = reinterpret_cast<CfrArena*>(pool + tb);
@@ -176,6 +176,14 @@ void cith_cfr_arena_reset_rows(uint8_t* pool, int B, int node_cap, int edge_cap,
   a->n_cap = (uint32_t)node_blocks;
   a->e_cap = (uint32_t)edge_blocks;
   a->row_cap = (uint32_t)row_cap;
+  a->pred = pred != 0;
+}
+void cith_cfr_arena_reset_rows(uint8_t* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                               int row_cap) {
+  cith_cfr_arena_reset_fmt(pool, B, node_cap, edge_cap, node_blocks, edge_blocks, row_cap, 1);
+}
+int64_t cith_cfr_arena_bytes_fmt(int node_blocks, int edge_blocks, int row_cap, int pred) {
+  return cfr_row_cap_ok(row_cap) ? cfr_arena_bytes(node_blocks, edge_blocks, row_cap, pred != 0) : -1;
 }
 void cith_cfr_arena_reset(uint8_t* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks) {
   cith_cfr_arena_reset_rows(pool, B, node_cap, edge_cap, node_blocks, edge_blocks, 0);

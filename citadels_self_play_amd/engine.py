@@ -106,11 +106,12 @@ def arena_blocks(B, node_cap, edge_cap, frac=None):
     return (min(B * nbt, max(nbt, math.ceil(fn * B * nbt))), min(B * ebt, max(ebt, math.ceil(fe * B * ebt))))
 
 
-def pool_bytes(B, node_cap, edge_cap, frac=None, row_cap="auto"):
-    """Device bytes of a B-tree node pool: per-tree regions + arena (cit_cfr.h)."""
+def pool_bytes(B, node_cap, edge_cap, frac=None, row_cap="auto", pred=False):
+    """Device bytes of a B-tree node pool: per-tree regions + arena (cit_cfr.h;
+    pred: room for pred_node_value, cfr_pred pools)."""
     nb, eb = arena_blocks(B, node_cap, edge_cap, frac)
     rc = row_cap_for(node_cap) if row_cap == "auto" else row_cap
-    return B * L.cfr_pool_bytes(node_cap, edge_cap) + L.cfr_arena_bytes(nb, eb, rc)
+    return B * L.cfr_pool_bytes(node_cap, edge_cap) + L.cfr_arena_bytes(nb, eb, rc, pred)
 
 
 def _ptr(t):
@@ -416,7 +417,7 @@ class GameBatch:
     arena_frac = None       # arena blocks as a fraction of the trees' worst case (arena_blocks)
     row_cap = "auto"        # row slot format: 0 raw rows, K diff rows (row_cap_for by node_cap)
 
-    def _pool(self, node_cap, edge_cap):
+    def _pool(self, node_cap, edge_cap, pred=False):
         """Node pool for B trees of (node_cap, edge_cap): block tables + an arena
         of arena_blocks(..., self.arena_frac) blocks, reset (empty) for a new
         search.  An arena that would not fit in device memory is cut to what
@@ -429,7 +430,7 @@ class GameBatch:
             raise ValueError("bad node pool capacity (%d nodes, %d edges)" % (node_cap, edge_cap))
         nb, eb = arena_blocks(self.B, node_cap, edge_cap, self.arena_frac)
         rc = row_cap_for(node_cap) if self.row_cap == "auto" else int(self.row_cap)
-        need = per * self.B + self.lib.cit_cfr_arena_bytes_rows(nb, eb, rc)
+        need = per * self.B + self.lib.cit_cfr_arena_bytes_fmt(nb, eb, rc, int(pred))
         have = self.pool.numel() if getattr(self, "pool", None) is not None else 0
         if need > have and self.device.type == "cuda":
             avail = int(0.9 * (torch.cuda.mem_get_info(self.device)[0] + have))
@@ -438,7 +439,7 @@ class GameBatch:
                 scale = max(0.0, (avail - per * self.B) / float(need - per * self.B))
                 nb0, eb0 = nb, eb
                 nb, eb = max(nbt, int(nb * scale)), max(ebt, int(eb * scale))
-                need = per * self.B + self.lib.cit_cfr_arena_bytes_rows(nb, eb, rc)
+                need = per * self.B + self.lib.cit_cfr_arena_bytes_fmt(nb, eb, rc, int(pred))
                 warnings.warn("node arena cut to %.0f%% of the requested %d node / %d edge blocks (%d trees): "
                               "device memory is short, trees that find it exhausted are searched again "
                               "(slower, same results); use fewer trees per batch to avoid this"
@@ -451,8 +452,8 @@ class GameBatch:
         if getattr(self, "optbuf", None) is None or self.optbuf.shape[0] != self.B:
             self.optbuf = torch.empty((self.B, self.lib.cit_cfr_opt_cap(), 16), dtype=torch.uint8, device=self.device)
         self.node_cap, self.edge_cap, self.arena, self.pool_row_cap = node_cap, edge_cap, (nb, eb), rc
-        _lib.check(self.lib.cit_cfr_arena_reset_rows(_ptr(self.pool), self.B, node_cap, edge_cap, nb, eb, rc,
-                                                     _stream()), "cit_cfr_arena_reset_rows")
+        _lib.check(self.lib.cit_cfr_arena_reset_fmt(_ptr(self.pool), self.B, node_cap, edge_cap, nb, eb, rc,
+                                                    int(pred), _stream()), "cit_cfr_arena_reset_fmt")
 
     def train_slice(self, iters, state, ticks, chosen, stats, running, flags=0):
         """One cit_cfr_train_slice launch over the pool bound by _pool (state [B,16]
@@ -519,7 +520,7 @@ class GameBatch:
 
     def _pred_begin(self, node_cap, edge_cap, orig):
         """Pool and per-tree buffers of a cfr_pred run (state, feat, probs, chosen, waiting)."""
-        self._pool(node_cap, edge_cap)
+        self._pool(node_cap, edge_cap, pred=True)
         self._model_tree = True
         d = self.device
         self._pred = {"o": self._orig(orig),

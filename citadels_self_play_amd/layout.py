@@ -96,7 +96,8 @@ def opt_from_bytes(b):
 # base row holding at most row_cap differing dwords.  tests/test_abi.py checks
 # these constants against the library (cit_cfr_block_sizes / cit_cfr_sizes).
 CFR_NB, CFR_EB, CFR_TBL_MAX = 4096, 16384, 1024
-CFR_NODE_BYTES, CFR_EDGE_BYTES, CFR_ARENA_HDR = 168, 48, 64
+CFR_NODE_BYTES, CFR_PRED_BYTES, CFR_EDGE_BYTES, CFR_ARENA_HDR = 72, 48, 48, 64
+NF_BACKED = 8                     # CfrNode flag: backpropagated (winning_probabilities = nv / nv.sum())
 CFR_ROW_W, CFR_ROW_HDR, CFR_ROW_MASKW, CFR_ROW_CAP_MAX = GAME_BYTES // 4, 16, 13, 368
 
 
@@ -122,8 +123,8 @@ def cfr_row_slot_bytes(row_cap=0):
     return 4 * (CFR_ROW_HDR + row_cap) if row_cap else GAME_BYTES
 
 
-def cfr_node_block_bytes(row_cap=0):
-    return CFR_NB * (CFR_NODE_BYTES + cfr_row_slot_bytes(row_cap))
+def cfr_node_block_bytes(row_cap=0, pred=True):
+    return CFR_NB * (CFR_NODE_BYTES + (CFR_PRED_BYTES if pred else 0) + cfr_row_slot_bytes(row_cap))
 
 
 def cfr_ring_bytes(n_blocks, e_blocks):
@@ -131,8 +132,8 @@ def cfr_ring_bytes(n_blocks, e_blocks):
     return (4 * (n_blocks + e_blocks) + 15) // 16 * 16
 
 
-def cfr_arena_bytes(n_blocks, e_blocks, row_cap=0):
-    return CFR_ARENA_HDR + cfr_ring_bytes(n_blocks, e_blocks) + n_blocks * cfr_node_block_bytes(row_cap) + \
+def cfr_arena_bytes(n_blocks, e_blocks, row_cap=0, pred=True):
+    return CFR_ARENA_HDR + cfr_ring_bytes(n_blocks, e_blocks) + n_blocks * cfr_node_block_bytes(row_cap, pred) + \
         e_blocks * CFR_EB * CFR_EDGE_BYTES
 
 
@@ -146,19 +147,47 @@ def cfr_row_decode(slot, base):
     return out.view(np.uint8)
 
 
+# A node record as the tests and tools read it (round 3's full record): the
+# header, node_value, winning_probabilities (derived: nv / nv.sum() once the
+# node was backpropagated, else zeros) and pred_node_value (zeros in pools
+# without pred).
+FULL_NODE_BYTES = 24 + 3 * 48
+
+
+def _full_nodes(rec, pred):
+    import numpy as np
+    n = rec.shape[0] // CFR_NODE_BYTES
+    rec = rec[:n * CFR_NODE_BYTES].reshape(n, CFR_NODE_BYTES)
+    out = np.zeros((n, FULL_NODE_BYTES), np.uint8)
+    out[:, :CFR_NODE_BYTES] = rec
+    nv = np.ascontiguousarray(rec[:, 24:72]).view("<f8")
+    s = np.zeros(n)
+    for k in range(6):                           # numpy's order for 6 elements
+        s = s + nv[:, k]
+    backed = (rec[:, 16] & NF_BACKED) != 0     # flags byte
+    with np.errstate(divide="ignore", invalid="ignore"):
+        wp = np.where(backed[:, None], nv / s[:, None], 0.0)
+    out[:, 72:120] = np.ascontiguousarray(wp).view(np.uint8).reshape(n, 48)
+    if pred is not None:
+        out[:, 120:168] = pred[:n * CFR_PRED_BYTES].reshape(n, CFR_PRED_BYTES)
+    return out.reshape(-1)
+
+
 def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
     """(node records, edge slots, game rows) of tree `lane` as uint8 arrays
-    gathered from its blocks in id order; `read(offset, nbytes)` returns pool
-    bytes as a uint8 ndarray (host pool or device copy)."""
+    gathered from its blocks in id order (node records in FULL_NODE_BYTES
+    form); `read(offset, nbytes)` returns pool bytes as a uint8 ndarray (host
+    pool or device copy)."""
     import numpy as np
     per = cfr_pool_bytes(node_cap, edge_cap)
     nb, eb = cfr_nblocks(node_cap), cfr_eblocks(edge_cap)
     tbl = np.array(read(lane * per, 4 * (nb + eb))).view("<i4")
     hdr = np.array(read(B * per, 48)).view("<u4")
-    n_cap, e_cap, row_cap = int(hdr[1]), int(hdr[3]), int(hdr[8])
+    n_cap, e_cap, row_cap, has_pred = int(hdr[1]), int(hdr[3]), int(hdr[8]), int(hdr[9])
     slot = cfr_row_slot_bytes(row_cap)
     node_base = B * per + CFR_ARENA_HDR + cfr_ring_bytes(n_cap, e_cap)
-    row_base = node_base + n_cap * CFR_NB * CFR_NODE_BYTES
+    pred_base = node_base + n_cap * CFR_NB * CFR_NODE_BYTES
+    row_base = pred_base + (n_cap * CFR_NB * CFR_PRED_BYTES if has_pred else 0)
     edge_base = row_base + n_cap * CFR_NB * slot
 
     def held(t):
@@ -174,7 +203,8 @@ def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
         return np.concatenate(parts) if parts else np.zeros(0, np.uint8)
 
     nbl, ebl = held(tbl[:nb]), held(tbl[nb:])
-    nodes = gather(node_base, CFR_NB * CFR_NODE_BYTES, nbl)
+    nodes = _full_nodes(gather(node_base, CFR_NB * CFR_NODE_BYTES, nbl),
+                        gather(pred_base, CFR_NB * CFR_PRED_BYTES, nbl) if has_pred else None)
     rows = gather(row_base, CFR_NB * slot, nbl).reshape(-1, slot)
     if row_cap:
         base = np.array(read(lane * per + cfr_tables_bytes(node_cap, edge_cap), GAME_BYTES)).view("<u4")

@@ -300,7 +300,7 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
         S2 = min(Q, int(S * overcommit))
         from .engine import row_cap_for
         scale = (max_pool_bytes - S2 * L.cfr_pool_bytes(node_cap, edge_cap)) / float(
-            L.cfr_arena_bytes(int(nb0), int(eb0), row_cap_for(node_cap)))
+            L.cfr_arena_bytes(int(nb0), int(eb0), row_cap_for(node_cap), False))
         S, arena_f = S2, (min(1.0, nb0 * scale / (S2 * nbt)), min(1.0, eb0 * scale / (S2 * ebt)))
     else:
         overcommit = 1.0

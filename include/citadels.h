@@ -178,8 +178,9 @@ int cit_mlp_forward_packed(const float* feat, int M, const void* packed, float* 
 /* Node pools.  A pool of B trees = B per-tree regions (cit_cfr_pool_bytes
  * each: int32 node-block and edge-block tables for node_cap / edge_cap,
  * padded to 16 B, then the tree's base row and a scratch row) followed by one
- * arena (cit_cfr_arena_bytes_rows(node_blocks, edge_blocks, row_cap)): a
- * 64-byte header, node blocks (CFR_NB CfrNode records of 168 B + CFR_NB row
+ * arena (cit_cfr_arena_bytes_fmt(node_blocks, edge_blocks, row_cap, pred)): a
+ * 64-byte header, node blocks (CFR_NB CfrNode records of 72 B: header +
+ * node_value f64[6]; with pred, CFR_NB pred_node_value f64[6]; CFR_NB row
  * slots, 16-byte aligned) and edge blocks (CFR_EB CfrEdge slots of 48 B),
  * after a ring of free block ids per kind.  A row slot holds a node's packed
  * game row raw (row_cap 0: CIT_GAME_BYTES) or as a diff against the tree's
@@ -196,7 +197,9 @@ int cit_mlp_forward_packed(const float* feat, int M, const void* packed, float* 
  * table longer than out[2] of cit_cfr_block_sizes). */
 int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap);
 int64_t cit_cfr_arena_bytes_rows(int node_blocks, int edge_blocks, int row_cap);
-int64_t cit_cfr_arena_bytes(int node_blocks, int edge_blocks);     /* = ..._rows(.., 0): raw rows */
+int64_t cit_cfr_arena_bytes_fmt(int node_blocks, int edge_blocks, int row_cap, int pred);
+int64_t cit_cfr_arena_bytes(int node_blocks, int edge_blocks);     /* = ..._rows(.., 0): raw rows
+                                                                     (_rows: with pred_node_value room) */
 /* out[3] = {CFR_NB nodes per node block, CFR_EB edges per edge block,
  * table entries a tree may hold}. */
 int cit_cfr_block_sizes(int32_t* out);
@@ -206,6 +209,12 @@ int cit_cfr_block_sizes(int32_t* out);
  * cit_cfr_arena_bytes_rows(...) bytes.  cit_cfr_arena_reset = row_cap 0. */
 int cit_cfr_arena_reset_rows(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
                              int row_cap, hipStream_t stream);
+/* The same with the node-record format too: pred != 0 gives every node room
+ * for pred_node_value (the pools of cfr_pred searches; cit_cfr_arena_reset /
+ * _rows reserve it), pred == 0 keeps records at 72 B (cfr_train searches,
+ * simulate_game's tree queue). */
+int cit_cfr_arena_reset_fmt(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
+                            int row_cap, int pred, hipStream_t stream);
 int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
                         hipStream_t stream);
 int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */

@@ -88,10 +88,10 @@ WIDE_DT = np.dtype([("R", "<f8", 6), ("S", "<f8", 6), ("CS", "<f8", 6)])
 assert NODE_DT.itemsize == 168 and EDGE_DT.itemsize == 48 and WIDE_DT.itemsize == 3 * 48
 
 
-def cfr_pool_bytes(node_cap, edge_cap, B=1, row_cap=0):
+def cfr_pool_bytes(node_cap, edge_cap, B=1, row_cap=0, pred=True):
     """A host pool of B trees with the worst-case arena (layout.cfr_* / cit_cfr.h)."""
     return B * L.cfr_pool_bytes(node_cap, edge_cap) + \
-        L.cfr_arena_bytes(B * L.cfr_nblocks(node_cap), B * L.cfr_eblocks(edge_cap), row_cap)
+        L.cfr_arena_bytes(B * L.cfr_nblocks(node_cap), B * L.cfr_eblocks(edge_cap), row_cap, pred)
 
 
 def node_arrays(nodes, edges, n):
@@ -111,14 +111,14 @@ def node_arrays(nodes, edges, n):
 class HostCfr:
     """Host-build MCCFR decisions over a HostBatch (config-3 harness)."""
 
-    def __init__(self, hb, node_cap=2048, edge_cap=4096, row_cap=0):
+    def __init__(self, hb, node_cap=2048, edge_cap=4096, row_cap=0, pred=True):
         self.hb = hb
         B = hb.B
-        self.node_cap, self.edge_cap, self.row_cap = node_cap, edge_cap, row_cap
+        self.node_cap, self.edge_cap, self.row_cap, self.pred = node_cap, edge_cap, row_cap, pred
         self.npmt = np.zeros((L.MT_N, B), np.uint32)
         self.npidx = np.zeros(B, np.uint32)
         lib().cith_mt_seed(_p(self.npmt), _p(self.npidx), C.c_int(B), _p(hb.seeds), C.c_int(1))
-        self.pool = np.zeros(cfr_pool_bytes(node_cap, edge_cap, B, row_cap), np.uint8)
+        self.pool = np.zeros(cfr_pool_bytes(node_cap, edge_cap, B, row_cap, pred), np.uint8)
         self.optbuf = np.zeros((B, 512, 16), np.uint8)
 
     def advance(self, lo, hi):
@@ -131,9 +131,10 @@ class HostCfr:
     def reset(self):
         """Empty block tables and arena (before each search; cfr_pred resumptions keep them)."""
         B = self.hb.B
-        lib().cith_cfr_arena_reset_rows(_p(self.pool), C.c_int(B), C.c_int(self.node_cap), C.c_int(self.edge_cap),
-                                        C.c_int(B * L.cfr_nblocks(self.node_cap)),
-                                        C.c_int(B * L.cfr_eblocks(self.edge_cap)), C.c_int(self.row_cap))
+        lib().cith_cfr_arena_reset_fmt(_p(self.pool), C.c_int(B), C.c_int(self.node_cap), C.c_int(self.edge_cap),
+                                       C.c_int(B * L.cfr_nblocks(self.node_cap)),
+                                       C.c_int(B * L.cfr_eblocks(self.edge_cap)), C.c_int(self.row_cap),
+                                       C.c_int(int(self.pred)))
 
     def decide(self, iters, flags=0):
         hb = self.hb

@@ -53,7 +53,14 @@ def test_cfr_pool_layout(lib):
     for rc in (0, 4, 128, 368):                               # diff row slots: 16 header words + rc dwords
         assert lib.cit_cfr_arena_bytes_rows(172, 17, rc) == L.cfr_arena_bytes(172, 17, rc) == \
             h.cith_cfr_arena_bytes_rows(172, 17, rc)
-    assert L.cfr_node_block_bytes(128) == 4096 * (168 + 576) < L.cfr_node_block_bytes(0) == 4096 * (168 + 1552)
+    assert L.cfr_node_block_bytes(128, False) == 4096 * (72 + 576) < L.cfr_node_block_bytes(0) == \
+        4096 * (72 + 48 + 1552)                               # 72-B records (+ pred_node_value in pred pools)
+    h.cith_cfr_arena_bytes_fmt.restype = C.c_int64
+    for rc in (0, 128):
+        for pred in (0, 1):
+            assert lib.cit_cfr_arena_bytes_fmt(172, 17, rc, pred) == L.cfr_arena_bytes(172, 17, rc, bool(pred)) == \
+                h.cith_cfr_arena_bytes_fmt(172, 17, rc, pred)
+    assert lib.cit_cfr_arena_bytes_fmt(1, 1, 130, 0) == -1
     for bad in (-4, 3, 130, 372):
         assert lib.cit_cfr_arena_bytes_rows(1, 1, bad) == -1
         assert lib.cit_cfr_arena_reset_rows(None, 4, 16, 16, 1, 1, bad, None) == -1
@@ -68,9 +75,10 @@ def test_arena_blocks():
     assert arena_blocks(10, 700_512, 2_806_144) == (1720, 1720)
     assert arena_blocks(10, 700_512, 2_806_144, (0.5, 0.8)) == (860, 1376)
     assert arena_blocks(1, 100, 500, 0.1) == (1, 1)           # never below one tree's worst case
-    assert pool_bytes(2, 100, 500) == 2 * (16 + 2 * 1552) + L.cfr_arena_bytes(2, 2)
+    assert pool_bytes(2, 100, 500) == 2 * (16 + 2 * 1552) + L.cfr_arena_bytes(2, 2, 0, False)
+    assert pool_bytes(2, 100, 500, pred=True) == 2 * (16 + 2 * 1552) + L.cfr_arena_bytes(2, 2)
     assert pool_bytes(2, 700_512, 2_806_144) == 2 * L.cfr_pool_bytes(700_512, 2_806_144) + \
-        L.cfr_arena_bytes(344, 344, 128)                       # large trees: diff row slots
+        L.cfr_arena_bytes(344, 344, 128, False)                # large trees: diff row slots, no pred
 
 
 def test_bad_args_rejected(lib):

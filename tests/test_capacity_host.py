@@ -29,7 +29,7 @@ def test_museum_past_16_matches_reference():
     for l, r in enumerate(recs):
         assert canon.canon_game(hb.game(l)) == r["position"], r["seed"]
     nc, ec = pool_caps(200_000)
-    cf = HostCfr(hb, node_cap=nc, edge_cap=ec, row_cap=128)
+    cf = HostCfr(hb, node_cap=nc, edge_cap=ec, row_cap=128, pred=False)     # the queue's pool format
     chosen, stats = cf.decide(200_000)
     per = split_targets(cfr_targets(cf, stats[:, 0], mode=2))
     for l, r in enumerate(recs):

@@ -21,7 +21,7 @@ def test_host_targets_match_reference(mode, row_cap):                    # 128: 
     random_position(hb, 100)
     for l, r in enumerate(recs):
         assert canon.canon_game(hb.game(l)) == r["position"], r["seed"]
-    cf = HostCfr(hb, node_cap=8192, edge_cap=8 * 8192, row_cap=row_cap)
+    cf = HostCfr(hb, node_cap=8192, edge_cap=8 * 8192, row_cap=row_cap, pred=row_cap == 0)   # 72-B records too
     chosen, stats = cf.decide(2000)
     t = cfr_targets(cf, stats[:, 0], mode=mode)
     per = split_targets(t)

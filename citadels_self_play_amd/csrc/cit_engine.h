@@ -1934,9 +1934,10 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
         area_splice(g, T, AL_HAND, 0, nt, np, [p0, p1](int i) { return i < 64 ? p0 : p1; });
       }
 #else
-      {   // swap the common prefix in place, then move the longer hand's rest over
-          // one card at a time (no private copy of a hand)
-        const int m = np < nt ? np : nt;
+      {   // swap the common prefix in place, append the longer hand's rest to the
+          // other, then cut it from the longer one in one splice (no private copy
+          // of a hand; the bytes left past the area are the wave path's)
+        const int m = np < nt ? np : nt, d = (np < nt ? nt : np) - m;
         for (int i = 0; i < m; i++) {
           uint8_t c = P.hand[i];
           P.hand[i] = T.hand[i];
@@ -1944,10 +1945,10 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
         }
         CitPlayer& A = np < nt ? P : T;     // receives the extra cards
         CitPlayer& Z = np < nt ? T : P;
-        for (int i = m; i < (np < nt ? nt : np); i++) {
-          const int c = Z.hand[m];
-          area_splice(g, Z, AL_HAND, m, 1, 0, [](int) { return 0; });
-          pl_put(g, A, AL_HAND, c);
+        if (area_used(A) + d > CIT_AREA_CAP) g.err |= CIT_ERR_OVERFLOW;
+        else {
+          for (int i = 0; i < d; i++) pl_put(g, A, AL_HAND, Z.hand[m + i]);
+          area_splice(g, Z, AL_HAND, m, d, 0, [](int) { return 0; });
         }
       }
 #endif

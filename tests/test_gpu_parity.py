@@ -260,7 +260,11 @@ def test_gpu_rollout_u_option_overflow(engine):
     rows_a = a.rows()
     c = engine(seeds, preset=False)
     sc, wc = c.rollout(games_per_block=8)
-    assert np.array_equal(c.rows(), rows_a)
+    rows_c = c.rows()
+    bad = np.nonzero((rows_c != rows_a).any(axis=1))[0]
+    assert len(bad) == 0, [(int(l), np.nonzero(rows_c[l] != rows_a[l])[0][:12].tolist(),
+                            canon.canon_game(L.game_from_bytes(rows_c[l])) == canon.canon_game(L.game_from_bytes(rows_a[l])))
+                           for l in bad[:6]]
     assert np.array_equal(sc.cpu().numpy(), sa) and np.array_equal(wc.cpu().numpy(), wa)
     big_draws = 0
     for l, s in enumerate(seeds):

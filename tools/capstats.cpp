@@ -12,6 +12,7 @@
 #define CIT_CAP_STATS 1
 #include "../citadels_self_play_amd/csrc/cit_host.cpp"
 
+#include <algorithm>
 #include <cstdio>
 #include <mutex>
 
@@ -70,6 +71,7 @@ int main(int argc, char** argv) {
   std::vector<int> hist[K_N];
   for (auto& h : hist) h.assign(256, 0);
   long long errs = 0, carry = 0;
+  std::vector<int> per_tree_carry(n, 0);
   auto work = [&]() {
     CitGame* g = (CitGame*)aligned_alloc(16, CIT_GAME_BYTES);
     uint8_t* pool = (uint8_t*)malloc((size_t)pool_bytes);
@@ -114,6 +116,7 @@ int main(int argc, char** argv) {
       }
       errs += st[4] != 0;
       carry += st[3];
+      per_tree_carry[i] = st[3];
       if (past) {
         printf("{\"seed\": %llu, \"err\": %d, \"carry_outs\": %d", (unsigned long long)seed, st[4], st[3]);
         for (int k = 0; k < K_N; k++) printf(", \"%s\": %d", kNames[k], tl_max[k]);
@@ -139,6 +142,11 @@ int main(int argc, char** argv) {
       }
     printf("}}\n");
   }
-  printf("{\"trees\": %d, \"iters\": %d, \"error_trees\": %lld, \"carry_outs\": %lld}\n", n, iters, errs, carry);
+  std::vector<int> sc = per_tree_carry;
+  std::sort(sc.begin(), sc.end());
+  auto pct = [&](double q) { return sc[(size_t)(q * (sc.size() - 1))]; };
+  printf("{\"trees\": %d, \"iters\": %d, \"error_trees\": %lld, \"carry_outs\": %lld, \"carry_outs_per_tree\": "
+         "{\"p10\": %d, \"p50\": %d, \"p90\": %d, \"p99\": %d, \"max\": %d}}\n",
+         n, iters, errs, carry, pct(0.1), pct(0.5), pct(0.9), pct(0.99), sc.back());
   return 0;
 }

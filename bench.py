@@ -250,9 +250,16 @@ def _pmc_pass(counters, outdir, config=2, timeout_s=150, cfr_child=False):
     rows = _rows(os.path.join(outdir, "**", "*counter_collection.csv"))
     if cfr_child:
         out = {}
+        # the child runs configs 3, 4, 5 in that order: config 3's k_cfr_decide
+        # dispatches precede config 4's first (config 5's overflow retries, if
+        # any, also launch k_cfr_decide: they come after)
+        c4 = [int(r["Dispatch_Id"]) for r in rows if KERNELS[4] in r.get("Kernel_Name", "") and "Dispatch_Id" in r]
+        first4 = min(c4) if c4 else None
         for kernel in (KERNELS[3], KERNELS[4], KERNELS[5]):
             per = {}
             for r in rows:
+                if kernel == KERNELS[3] and first4 is not None and int(r.get("Dispatch_Id", "0")) > first4:
+                    continue
                 if kernel in r.get("Kernel_Name", ""):
                     per.setdefault(r["Counter_Name"], {}).setdefault(r.get("Dispatch_Id", "0"), 0.0)
                     per[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
@@ -298,7 +305,10 @@ def pmc_in_run(config=2):
 # Counter passes over one --pmc-child run of the three search workloads (their
 # kernels are distinct, so one child serves configs 3, 4 and 5).
 CFR_PMC_PASSES = (["FETCH_SIZE"], ["WRITE_SIZE"], SQ_SET, ["SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"])
-PMC_CHILD = {3: 1024, 4: 4096, 5: 128}          # positions / trees per config in the --pmc-child run
+# positions / trees per config in the --pmc-child run.  Config 5 runs at its
+# bench size: fewer trees fit in HBM at once and would search in k_cfr_decide
+# (simulate_games without the queue), not in the queue's k_cfr_train_slice.
+PMC_CHILD = {3: 1024, 4: 4096, 5: 1920}
 
 
 def pmc_in_run_cfr():

@@ -57,7 +57,7 @@ struct CfrNode {                       // 72 B
   uint8_t flags;
   int8_t winner;
   int16_t sib;                         // index among the parent's children (-1: root)
-  uint8_t pad[4];
+  int32_t row;                         // diff-row pools: edge index of the node's row run (else unused)
   double nv[6];
 };
 #define CFR_PRED_BYTES 48              // pred_node_value f64[6] per node (cfr_pred pools)
@@ -98,17 +98,19 @@ static_assert(sizeof(CfrWide) == 3 * sizeof(CfrEdge), "CfrWide layout");
 //     uint32 [n_cap] + [e_cap] (padded to 16 B) | node records [n_cap
 //     blocks][CFR_NB] | node row slots [n_cap blocks][CFR_NB] (16-byte
 //     aligned) | edges [e_cap blocks][CFR_EB]
-// Row slots (the arena's row_cap, cfr_row_slot_bytes): row_cap 0 stores each
-// node's game row raw (CIT_GAME_BYTES); row_cap K > 0 stores it as a diff
-// against the tree's base row (its root game as first created): a header of
-// CFR_ROW_HDR words (bit d of the 388-bit mask in words 0..12 = dword d differs
-// from the base; word 13 the count) and then the differing dwords in index
-// order, at most K.  A cfr_train(200000) node differs from its root in ~70 of
-// 388 dwords (max ~100 measured), so K = 128 cuts a node's record + row slot
-// from 1,720 to 744 B (0.43x; with its ~4 edge slots 1.9 KB -> 0.94 KB); a row
-// with more than K differing dwords stops the tree with CIT_ERR_OVERFLOW and
-// the tree is searched again with raw rows (engine.py's retry): the slot size
-// never changes a result.
+// Node rows (the arena's row_cap): row_cap 0 stores each node's game row raw
+// (CIT_GAME_BYTES) in a row slot of its node block.  row_cap K > 0 stores it
+// as a diff against the tree's base row (its root game as first created), of
+// the length it has, in the tree's edge space: a run of cfr_row_slots(k) edge
+// slots (CfrNode.row) holding a header of CFR_ROW_HDR words (bit d of the
+// 388-bit mask in words 0..12 = dword d differs from the base; word 13 the
+// count k) and then the k differing dwords in index order; node blocks then
+// hold records only.  A cfr_train(200000) node differs from its root in ~70
+// of 388 dwords (~7 edge slots, 336 B, against a fixed 128-dword slot's 576 B
+// and a raw row's 1,552 B).  A row with more than K differing dwords stops the
+// tree with CIT_ERR_OVERFLOW | CIT_ERR_POOL_ROW and the tree is searched again
+// with raw rows (engine.py's retry; K = 388, the product's, never overflows):
+// the format never changes a result.
 // A block is taken from its free ring (blocks released by finished trees,
 // cit_cfr_arena_release) or, when that is empty, from the never-used rest.
 // Node id n lives in block nbt[n >> CFR_NB_SHIFT] at slot n & (CFR_NB - 1);
@@ -127,9 +129,9 @@ struct CfrArena {                             // 64 B, written by cit_cfr_arena_
   uint32_t pad[6];
 };
 #define CFR_ROW_W (CIT_GAME_BYTES / 4)        // 388 dwords
-#define CFR_ROW_HDR 16                        // header words of a diff row slot
+#define CFR_ROW_HDR 14                        // header words of a diff row run (mask, count)
 #define CFR_ROW_MASKW 13                      // mask words (388 bits)
-#define CFR_ROW_CAP_MAX 368                   // a diff slot must stay below a raw row
+#define CFR_ROW_CAP_MAX CFR_ROW_W             // every dword may differ
 static_assert(sizeof(CfrArena) == 64, "CfrArena layout");
 
 struct CfrTree {
@@ -166,6 +168,13 @@ struct CfrTree {
   // child's expansion (which asks for its parent's player and state) do not
   // read the record from HBM again.  cur_node -1: nothing cached.
   int cur_node, cur_fe, cur_nch, cur_flags, cur_player, cur_state;
+  // Diff-row pools: the row run of node rn_node (read with its header by
+  // cfr_expand / cfr_update_strategy, so row_load needs no read of the
+  // record), and the run and its capacity (in differing dwords) of the row
+  // row_load or row_store last handled (rl_node), which a re-store of that
+  // node reuses when the new diff fits.  -1: none.
+  int rn_node, rn_run;
+  int rl_node, rl_run, rl_k;
 };
 
 CIT_HD int cfr_nblocks(int node_cap) { return (node_cap + CFR_NB - 1) >> CFR_NB_SHIFT; }
@@ -177,8 +186,11 @@ CIT_HD int64_t cfr_pool_bytes(int node_cap, int edge_cap) {   // per tree: table
   return cfr_tables_bytes(node_cap, edge_cap) + 2 * (int64_t)CIT_GAME_BYTES;
 }
 CIT_HD int cfr_row_cap_ok(int row_cap) { return row_cap == 0 || (row_cap > 0 && row_cap <= CFR_ROW_CAP_MAX && !(row_cap & 3)); }
-CIT_HD int64_t cfr_row_slot_bytes(int row_cap) {
-  return row_cap > 0 ? (int64_t)4 * (CFR_ROW_HDR + row_cap) : (int64_t)CIT_GAME_BYTES;
+// bytes of a node block's row slot: a raw row, none for diff rows (they live in edge space)
+CIT_HD int64_t cfr_row_slot_bytes(int row_cap) { return row_cap > 0 ? 0 : (int64_t)CIT_GAME_BYTES; }
+// edge slots of a diff row run with k differing dwords
+CIT_HD int cfr_row_slots(int k) {
+  return (CFR_ROW_HDR + k + (int)(sizeof(CfrEdge) / 4) - 1) / (int)(sizeof(CfrEdge) / 4);
 }
 CIT_HD int64_t cfr_node_block_bytes(int row_cap = 0, int pred = 1) {
   return (int64_t)CFR_NB * ((int64_t)sizeof(CfrNode) + (pred ? CFR_PRED_BYTES : 0) + cfr_row_slot_bytes(row_cap));
@@ -210,6 +222,7 @@ CIT_HD void cfr_tree_bind(CfrTree& T, uint8_t* pool, int B, long l, int node_cap
   T.node_cap = node_cap;
   T.edge_cap = edge_cap;
   T.cur_node = -1;
+  T.rn_node = T.rl_node = -1;
 }
 // Resumable cfr_pred state of one tree (see cfr_pred_run below): 64 B,
 // persists in HBM between launches.
@@ -402,6 +415,19 @@ CIT_HD CfrWide* cfr_wide(const CfrTree& T, int first_edge) {
 CIT_HD uint32_t* row_of(const CfrTree& T, int id) {
   return reinterpret_cast<uint32_t*>(cfr_glb(T.row_base) + cfr_node_slot(T, id) * T.row_slot);
 }
+// A run of n edge slots (a node's children, or a diff row) inside one edge block.
+CIT_HD int alloc_edges(CfrTree& T, int n) {
+  int f = T.n_edges;
+  if ((f & (CFR_EB - 1)) + n > CFR_EB) f = (f | (CFR_EB - 1)) + 1;
+  if (f + n > T.edge_cap) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_CAP; return -1; }
+  while (((f + n - 1) >> CFR_EB_SHIFT) >= T.n_eblk) {
+    int b = cfr_take_block(cfr_glb(T.arena), 1);
+    if (b < 0) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_ARENA; return -1; }
+    cfr_ebt_at(T, T.n_eblk++) = b;
+  }
+  T.n_edges = f + n;
+  return f;
+}
 CIT_HD uint32_t* w_row(const CfrTree& T, int which) { return reinterpret_cast<uint32_t*>(&cfr_w(T, which)); }
 
 // One out-of-line copy of each engine entry point for the search: the
@@ -505,43 +531,45 @@ __device__ __forceinline__ uint32_t cfr_mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 #endif
-CIT_HD void row_load(const CfrTree& T, uint32_t* dst, int id) {
-  const uint32_t* s = row_of(T, id);
+// The row run of node id (diff-row pools): the cached one when id's header was
+// just read, else from its record.
+CIT_HD int row_run_of(const CfrTree& T, int id) {
+  return cfr_u(T.rn_node) == id ? cfr_u(T.rn_run) : cfr_node(T, id).row;
+}
+CIT_HD uint32_t* row_run_ptr(const CfrTree& T, int run) { return reinterpret_cast<uint32_t*>(cfr_edge(T, run)); }
+CIT_HD void row_load(CfrTree& T, uint32_t* dst, int id) {
   if (cfr_u(T.row_cap) == 0) {
-    copy_row(T, dst, s);
+    copy_row(T, dst, row_of(T, id));
     return;
   }
+  const int run = cfr_u(row_run_of(T, id));
+  const uint32_t* s = row_run_ptr(T, run);
   const uint32_t* base = cfr_base(T);
+  uint32_t k;
   CFR_SYNC();
 #if CIT_WAVE
-  if (cfr_u(T.row_cap) + CFR_ROW_HDR <= 4 * 64) {
-    // the whole slot in one round of loads (up to 4 dwords per lane, more than
-    // the differing dwords need: latency, not bytes, bounds the search), staged
-    // in the LDS scratch so each lane can read its dwords' values by rank;
-    // lanes 0..12 hold the mask words, chunk j = dwords 64j..64j+63
-    const int l = CFR_LANE, nw = cfr_u(T.row_cap) + CFR_ROW_HDR;
+  {
+    // one round of loads: up to 4 dwords per lane from the run on (not past
+    // its edge block: a run never straddles one), which hold the whole row
+    // when it has at most 256 - CFR_ROW_HDR differing dwords, staged in the
+    // LDS scratch so each lane can read its dwords' values by rank; lanes
+    // 0..12 hold the mask words, lane 13 the count; chunk j = dwords 64j..64j+63
+    const int l = CFR_LANE;
+    const int left = (CFR_EB - (run & (CFR_EB - 1))) * (int)(sizeof(CfrEdge) / 4);
+    const int nw = left < 4 * 64 ? left : 4 * 64;
     uint32_t* stg = reinterpret_cast<uint32_t*>(cfr_ls.tmp);
     static_assert(4 * 64 * 4 <= CIT_SAMPLE_SCRATCH, "row staging fits the scratch");
     uint32_t v[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) v[k] = l + 64 * k < nw ? s[l + 64 * k] : 0u;
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (l + 64 * k < nw) stg[l + 64 * k] = v[k];
+    for (int q = 0; q < 4; q++) v[q] = l + 64 * q < nw ? s[l + 64 * q] : 0u;
     const uint32_t mw = v[0];
-    uint32_t acc = 0;
+    k = (uint32_t)cfr_u((int)__builtin_amdgcn_readlane((int)mw, CFR_ROW_MASKW));
+    const bool staged = CFR_ROW_HDR + (int)k <= nw;
+    if (staged) {
 #pragma unroll
-    for (int j = 0; j < (CFR_ROW_W + 63) / 64; j++) {
-      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mw, 2 * j);
-      const uint32_t hi = 2 * j + 1 < CFR_ROW_MASKW ? (uint32_t)__builtin_amdgcn_readlane((int)mw, 2 * j + 1) : 0u;
-      const uint64_t m = ((uint64_t)hi << 32) | lo;
-      const int d = 64 * j + l;
-      if (d < CFR_ROW_W) dst[d] = ((m >> l) & 1) ? stg[CFR_ROW_HDR + acc + cfr_mbcnt(m)] : base[d];
-      acc += (uint32_t)__popcll(m);
+      for (int q = 0; q < 4; q++)
+        if (l + 64 * q < CFR_ROW_HDR + (int)k) stg[l + 64 * q] = v[q];
     }
-  } else {   // lanes 0..12 hold the mask words; chunk j = dwords 64j..64j+63 on the 64 lanes
-    const int l = CFR_LANE;
-    const uint32_t mw = l < CFR_ROW_MASKW ? s[l] : 0u;
     uint32_t acc = 0;
 #pragma unroll
     for (int j = 0; j < (CFR_ROW_W + 63) / 64; j++) {
@@ -549,26 +577,38 @@ CIT_HD void row_load(const CfrTree& T, uint32_t* dst, int id) {
       const uint32_t hi = 2 * j + 1 < CFR_ROW_MASKW ? (uint32_t)__builtin_amdgcn_readlane((int)mw, 2 * j + 1) : 0u;
       const uint64_t m = ((uint64_t)hi << 32) | lo;
       const int d = 64 * j + l;
-      if (d < CFR_ROW_W) dst[d] = ((m >> l) & 1) ? s[CFR_ROW_HDR + acc + cfr_mbcnt(m)] : base[d];
+      if (d < CFR_ROW_W)
+        dst[d] = ((m >> l) & 1) ? (staged ? stg[CFR_ROW_HDR + acc + cfr_mbcnt(m)] : s[CFR_ROW_HDR + acc + cfr_mbcnt(m)])
+                                : base[d];
       acc += (uint32_t)__popcll(m);
     }
   }
 #else
   {
-    uint32_t k = 0;
+    k = s[CFR_ROW_MASKW];
+    uint32_t q = 0;
     for (int d = 0; d < CFR_ROW_W; d++)
-      dst[d] = ((s[d >> 5] >> (d & 31)) & 1) ? s[CFR_ROW_HDR + k++] : base[d];
+      dst[d] = ((s[d >> 5] >> (d & 31)) & 1) ? s[CFR_ROW_HDR + q++] : base[d];
   }
 #endif
+  T.rl_node = id;
+  T.rl_run = run;
+  T.rl_k = (int)k;
   CFR_SYNC();
 }
-CIT_HD void row_store(CfrTree& T, int id, const uint32_t* src) {
-  uint32_t* s = row_of(T, id);
+// Working row src as node id's row.  Raw rows: into the node's slot (returns
+// -1).  Diff rows: a new run (or, given reuse_run, that run when the diff
+// fits its reuse_k dwords) -- returns the run, -1 with T.err set when the
+// diff is past row_cap or edge space ran out.
+CIT_HD int row_store(CfrTree& T, int id, const uint32_t* src, int reuse_run = -1, int reuse_k = 0) {
   if (cfr_u(T.row_cap) == 0) {
-    copy_row(T, s, src);
-    return;
+    copy_row(T, row_of(T, id), src);
+    return -1;
   }
+  reuse_run = cfr_u(reuse_run);
+  reuse_k = cfr_u(reuse_k);
   const uint32_t* base = cfr_base(T);
+  int run = -1;
   CFR_SYNC();
 #if CIT_WAVE
   {
@@ -587,16 +627,24 @@ CIT_HD void row_store(CfrTree& T, int id, const uint32_t* src) {
     if (tot > (uint32_t)cfr_u(T.row_cap)) {
       T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_ROW;
     } else {
-      uint32_t acc = 0;
+      const bool reuse = reuse_run >= 0 && cfr_row_slots((int)tot) <= cfr_row_slots(reuse_k);
+      run = reuse ? reuse_run : cfr_u(alloc_edges(T, cfr_row_slots((int)tot)));
+      if (run >= 0) {
+        uint32_t* s = row_run_ptr(T, run);
+        uint32_t acc = 0;
 #pragma unroll
-      for (int j = 0; j < NJ; j++) {
-        if ((m[j] >> l) & 1) s[CFR_ROW_HDR + acc + cfr_mbcnt(m[j])] = v[j];
-        acc += (uint32_t)__popcll(m[j]);
+        for (int j = 0; j < NJ; j++) {
+          if ((m[j] >> l) & 1) s[CFR_ROW_HDR + acc + cfr_mbcnt(m[j])] = v[j];
+          acc += (uint32_t)__popcll(m[j]);
+        }
+        uint32_t h = l == CFR_ROW_MASKW ? tot : 0u;
+#pragma unroll
+        for (int w = 0; w < CFR_ROW_MASKW; w++) h = l == w ? (uint32_t)(m[w >> 1] >> (32 * (w & 1))) : h;
+        if (l < CFR_ROW_HDR) s[l] = h;
+        T.rl_node = id;
+        T.rl_run = run;
+        T.rl_k = reuse && reuse_k > (int)tot ? reuse_k : (int)tot;
       }
-      uint32_t h = l == CFR_ROW_MASKW ? tot : 0u;
-#pragma unroll
-      for (int w = 0; w < CFR_ROW_MASKW; w++) h = l == w ? (uint32_t)(m[w >> 1] >> (32 * (w & 1))) : h;
-      if (l < CFR_ROW_HDR) s[l] = h;
     }
   }
 #else
@@ -611,14 +659,40 @@ CIT_HD void row_store(CfrTree& T, int id, const uint32_t* src) {
     if (k > (uint32_t)T.row_cap) {
       T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_ROW;
     } else {
-      k = 0;
-      for (int d = 0; d < CFR_ROW_W; d++)
-        if ((mask[d >> 5] >> (d & 31)) & 1) s[CFR_ROW_HDR + k++] = src[d];
-      for (int w = 0; w < CFR_ROW_HDR; w++) s[w] = w < CFR_ROW_MASKW ? mask[w] : (w == CFR_ROW_MASKW ? k : 0u);
+      const bool reuse = reuse_run >= 0 && cfr_row_slots((int)k) <= cfr_row_slots(reuse_k);
+      run = reuse ? reuse_run : alloc_edges(T, cfr_row_slots((int)k));
+      if (run >= 0) {
+        uint32_t* s = row_run_ptr(T, run);
+        uint32_t q = 0;
+        for (int d = 0; d < CFR_ROW_W; d++)
+          if ((mask[d >> 5] >> (d & 31)) & 1) s[CFR_ROW_HDR + q++] = src[d];
+        for (int w = 0; w < CFR_ROW_HDR; w++) s[w] = w < CFR_ROW_MASKW ? mask[w] : k;
+        T.rl_node = id;
+        T.rl_run = run;
+        T.rl_k = reuse && reuse_k > (int)k ? reuse_k : (int)k;
+      }
     }
   }
 #endif
   CFR_SYNC();
+  return run;
+}
+// Node id's row := working row src for a node that has one (its game changed:
+// get_options' lazy state, a live choice): in place when row_load / row_store
+// last handled id and the diff fits its run, else in a new run the record
+// then points to.
+CIT_HD void row_restore(CfrTree& T, int id, const uint32_t* src) {
+  if (cfr_u(T.row_cap) == 0) {
+    row_store(T, id, src);
+    return;
+  }
+  const bool have = cfr_u(T.rl_node) == id;
+  const int old = have ? cfr_u(T.rl_run) : -1;
+  const int run = cfr_u(row_store(T, id, src, old, have ? cfr_u(T.rl_k) : 0));
+  if (run >= 0 && run != old) {
+    cfr_node(T, id).row = run;
+    if (cfr_u(T.rn_node) == id) T.rn_run = run;
+  }
 }
 // The tree's base row := working row src (its root game as first created), in
 // the pool and (device) in LDS.
@@ -631,7 +705,7 @@ CIT_HD void row_set_base(CfrTree& T, const uint32_t* src) {
 }
 // A read-only view of node n's game: the slot itself for raw rows, else the
 // row decompressed into working row `which` (device) / the tree's scratch row.
-CIT_HD const CitGame& row_view(const CfrTree& T, int n, int which) {
+CIT_HD const CitGame& row_view(CfrTree& T, int n, int which) {
   if (cfr_u(T.row_cap) == 0) return *reinterpret_cast<const CitGame*>(row_of(T, n));
 #if CIT_WAVE
   row_load(T, w_row(T, which), n);
@@ -864,6 +938,8 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
     cfr_nbt_at(T, id >> CFR_NB_SHIFT) = b;
   }
   T.n_nodes = id + 1;
+  if (id == 0) row_set_base(T, w_row(T, which));   // the root: the tree's base row
+  const int run = cfr_u(row_store(T, id, w_row(T, which)));   // its row (run: diff-row pools)
   CfrNode& N = cfr_node(T, id);
 #if CIT_WAVE
   {   // the header's 6 words and the 12 zero words of nv, one store per lane
@@ -874,7 +950,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
     hw[3] = (uint32_t)(uint16_t)depth | ((uint32_t)(uint8_t)w.gs_pid << 16) | ((uint32_t)w.gs_state << 24);
     hw[4] = (uint32_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0)) |
             ((uint32_t)(uint8_t)w.winner << 8) | 0xffff0000u;   // sib = -1 until the parent links it
-    hw[5] = 0;
+    hw[5] = (uint32_t)run;
     const int l = CFR_LANE;
     uint32_t v = 0;
     for (int k = 0; k < 6; k++) v = l == k ? hw[k] : v;
@@ -891,26 +967,12 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   N.flags = (uint8_t)((w.gs_state == 0 ? NF_ROLE_PICK : 0) | (w.terminal ? NF_TERMINAL : 0));
   N.winner = w.winner;
   N.sib = -1;
+  N.row = run;
   for (int k = 0; k < 6; k++) N.nv[k] = 0.0;
 #endif
-  if (id == 0) row_set_base(T, w_row(T, which));   // the root: the tree's base row
-  row_store(T, id, w_row(T, which));
   return id;
 }
 
-// A run of n edge slots (a node's children) inside one edge block.
-CIT_HD int alloc_edges(CfrTree& T, int n) {
-  int f = T.n_edges;
-  if ((f & (CFR_EB - 1)) + n > CFR_EB) f = (f | (CFR_EB - 1)) + 1;
-  if (f + n > T.edge_cap) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_CAP; return -1; }
-  while (((f + n - 1) >> CFR_EB_SHIFT) >= T.n_eblk) {
-    int b = cfr_take_block(cfr_glb(T.arena), 1);
-    if (b < 0) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_ARENA; return -1; }
-    cfr_ebt_at(T, T.n_eblk++) = b;
-  }
-  T.n_edges = f + n;
-  return f;
-}
 CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
   E.opt = o;
   E.child = child;
@@ -989,7 +1051,7 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n, int par, int player, int 
   int nl = lc.n;
   T.err |= lc.err | g.err;
   if (nl > CFR_OPT_CAP) T.err |= CIT_ERR_OVERFLOW;
-  row_store(T, n, w_row(T, 0));   // get_options mutated the node's game
+  row_restore(T, n, w_row(T, 0));   // get_options mutated the node's game
   if (T.err) return;
   int cnt = nl;
   int f = alloc_edges(T, cnt);
@@ -1068,6 +1130,8 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player,
 CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
   CfrNode& N = cfr_node(T, n);
   const int state = N.gs_state, nch = N.n_children, player = N.player, par = N.parent, depth = N.depth;
+  T.rn_node = n;
+  T.rn_run = N.row;
   if (state == 0 && nch == 0) {
     N.flags |= NF_ROLE_PICK;
     cfr_expand_role_pick(T, n, depth);
@@ -1091,6 +1155,8 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
   T.cur_flags = flags;
   T.cur_player = N.player;
   T.cur_state = N.gs_state;
+  T.rn_node = n;
+  T.rn_run = N.row;
   if (nch == 0) return;
   CfrEdge* E = cfr_edge(T, fe);
 #if CIT_WAVE
@@ -1436,7 +1502,7 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
   double sum = 0.0;
   for (int j = 0; j < nl; j++) sum += W[ob[j].a].S[pid];
   int j = np_choice(T.np, [&](int i) { return W[ob[i].a].S[pid] / sum; }, nl, T.err);
-  row_store(T, root, w_row(T, 0));
+  row_restore(T, root, w_row(T, 0));
   if (T.err || j < 0) return mk(O_NUM_NAMES, 0);
   return ob[j];
 }
@@ -1636,7 +1702,7 @@ CIT_HD void cfr_count_targets(const CfrTree& T, int root, int mode, int32_t& n_t
 //   feat[k][418] = encode_game (role-pick node: player randint(0, 5) of the tree's stream)
 //   value[k][6] = node_value;  regret rows dist[c0 + j] (role-pick: cumulative_regrets[i]),
 //   all ones when they sum to 0;  opt_feat[c0 + j][131] = encode_option of child j.
-CIT_HD void cfr_emit_targets(const CfrTree& T, CitMT& py, int root, int mode, int lane, int32_t t0, int32_t c0,
+CIT_HD void cfr_emit_targets(CfrTree& T, CitMT& py, int root, int mode, int lane, int32_t t0, int32_t c0,
                              int32_t* meta, float* feat, double* value, double* dist, float* opt_feat) {
   if (root < 0) return;
   int32_t t = t0, c = c0;

@@ -55,20 +55,25 @@ def node_arrays(nodes, edges, n):
 def pool_caps(iters):
     """Node / edge capacity for a cfr_train(iters) tree: measured 1.2-3.3 nodes
     per iteration (2000 iterations: up to 6,604 nodes; 200000: up to 646,897)
-    and 3.1-4.4 reserved edge slots per node; a tree that still outgrows its
-    pool is searched again with a 4x pool (GameBatch._retry_overflow)."""
+    and 3.1-4.4 reserved edge slots per node, plus ROW_EDGE_SLOTS per node for
+    the diff rows of large trees (row_cap_for: ~7 slots measured); a tree that
+    still outgrows its pool is searched again with a 4x pool
+    (GameBatch._retry_overflow).  Caps bound a tree; the arena holds what the
+    trees use."""
     node_cap = max(1024, int(3.5 * iters) + 512)
-    return node_cap, 4 * node_cap + 4096
+    rows = ROW_EDGE_SLOTS * node_cap if row_cap_for(node_cap) else 0
+    return node_cap, 4 * node_cap + 4096 + rows
 
 
-# Row slots of large trees' node pools: diffs against the tree's base row with
-# room for CFR_ROW_CAP differing dwords (cit_cfr.h; a cfr_train(200000) node
-# differs in ~70 of 388, at most ~100 measured): a node's record + row slot
-# go from 1,720 to 744 B (with its edge slots ~1.9 KB -> ~0.94 KB), so about
-# twice the trees fit in HBM (config 5: 688 -> 1,326 queue slots, DESIGN.md
-# §2).  A tree with a row past the cap is searched again
-# with raw rows (_retry_overflow).  Small trees (configs 3/4) keep raw rows.
-CFR_ROW_CAP = int(os.environ.get("CIT_ROW_CAP", "128"))      # (0: raw rows everywhere, for A/B runs)
+# Rows of large trees' node pools: diffs against the tree's base row, each a
+# run of edge slots as long as its diff (cit_cfr.h; a cfr_train(200000) node
+# differs in ~70 of 388 dwords: ~7 slots, 336 B, against round 3's fixed
+# 576-B slot and a raw row's 1,552 B), with at most CFR_ROW_CAP differing
+# dwords (388, the default: never past; a smaller cap is a testing aid whose
+# overflowing trees are searched again with raw rows, _retry_overflow).
+# Small trees (configs 3/4) keep raw rows.
+CFR_ROW_CAP = int(os.environ.get("CIT_ROW_CAP", str(L.CFR_ROW_W)))      # (0: raw rows everywhere, for A/B runs)
+ROW_EDGE_SLOTS = 10        # edge slots per node pool_caps reserves for its row run
 # cfr_pred splits batches of at least this many trees into 2 stream groups
 PRED_GROUP_MIN = int(os.environ.get("CIT_PRED_GROUP_MIN", "2048"))
 PRED_GROUPS = int(os.environ.get("CIT_PRED_GROUPS", "3"))

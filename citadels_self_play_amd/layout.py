@@ -90,15 +90,18 @@ def opt_from_bytes(b):
 
 
 # ---- MCCFR node pools (csrc/cit_cfr.h): B per-tree regions (block tables, base
-# row, scratch row), then one arena of node blocks (CFR_NB node records +
-# CFR_NB row slots) and edge blocks (CFR_EB edge slots) the trees take as they
-# grow.  Row slots are raw game rows (row_cap 0) or diffs against the tree's
-# base row holding at most row_cap differing dwords.  tests/test_abi.py checks
-# these constants against the library (cit_cfr_block_sizes / cit_cfr_sizes).
+# row, scratch row), then one arena of node blocks (CFR_NB node records, and
+# CFR_NB raw row slots in row_cap-0 pools) and edge blocks (CFR_EB edge slots)
+# the trees take as they grow.  Rows are raw game rows (row_cap 0) or diffs
+# against the tree's base row with at most row_cap differing dwords, each a
+# run of edge slots (CfrNode.row: a CFR_ROW_HDR-word header, then the
+# differing dwords).  tests/test_abi.py checks these constants against the
+# library (cit_cfr_block_sizes / cit_cfr_sizes).
 CFR_NB, CFR_EB, CFR_TBL_MAX = 4096, 16384, 1024
 CFR_NODE_BYTES, CFR_PRED_BYTES, CFR_EDGE_BYTES, CFR_ARENA_HDR = 72, 48, 48, 64
 NF_BACKED = 8                     # CfrNode flag: backpropagated (winning_probabilities = nv / nv.sum())
-CFR_ROW_W, CFR_ROW_HDR, CFR_ROW_MASKW, CFR_ROW_CAP_MAX = GAME_BYTES // 4, 16, 13, 368
+CFR_ROW_W, CFR_ROW_HDR, CFR_ROW_MASKW = GAME_BYTES // 4, 14, 13
+CFR_ROW_CAP_MAX = CFR_ROW_W
 
 
 def cfr_nblocks(node_cap):
@@ -120,7 +123,13 @@ def cfr_pool_bytes(node_cap, edge_cap):
 
 
 def cfr_row_slot_bytes(row_cap=0):
-    return 4 * (CFR_ROW_HDR + row_cap) if row_cap else GAME_BYTES
+    """A node block's row slot: a raw row; none in diff-row pools (their rows are edge-slot runs)."""
+    return 0 if row_cap else GAME_BYTES
+
+
+def cfr_row_slots(k):
+    """Edge slots of a diff row run with k differing dwords."""
+    return -(-(CFR_ROW_HDR + int(k)) // (CFR_EDGE_BYTES // 4))
 
 
 def cfr_node_block_bytes(row_cap=0, pred=True):
@@ -138,7 +147,7 @@ def cfr_arena_bytes(n_blocks, e_blocks, row_cap=0, pred=True):
 
 
 def cfr_row_decode(slot, base):
-    """A diff row slot (uint8 [slot bytes]) against the tree's base row -> the game row."""
+    """A diff row run (uint8, from its first slot on) against the tree's base row -> the game row."""
     import numpy as np
     w = np.asarray(slot).view("<u4")
     mask = np.unpackbits(w[:CFR_ROW_MASKW].view(np.uint8), bitorder="little")[:CFR_ROW_W].astype(bool)
@@ -203,16 +212,24 @@ def cfr_tree_bytes(read, B, lane, node_cap, edge_cap):
         return np.concatenate(parts) if parts else np.zeros(0, np.uint8)
 
     nbl, ebl = held(tbl[:nb]), held(tbl[nb:])
-    nodes = _full_nodes(gather(node_base, CFR_NB * CFR_NODE_BYTES, nbl),
-                        gather(pred_base, CFR_NB * CFR_PRED_BYTES, nbl) if has_pred else None)
-    rows = gather(row_base, CFR_NB * slot, nbl).reshape(-1, slot)
-    if row_cap:
-        base = np.array(read(lane * per + cfr_tables_bytes(node_cap, edge_cap), GAME_BYTES)).view("<u4")
-        w = np.ascontiguousarray(rows).view("<u4")
+    rec = gather(node_base, CFR_NB * CFR_NODE_BYTES, nbl)
+    nodes = _full_nodes(rec, gather(pred_base, CFR_NB * CFR_PRED_BYTES, nbl) if has_pred else None)
+    edges = gather(edge_base, CFR_EB * CFR_EDGE_BYTES, ebl)
+    if not row_cap:
+        rows = gather(row_base, CFR_NB * slot, nbl).reshape(-1, slot)
+        return nodes, edges, rows
+    # diff rows: node i's run starts at edge slot CfrNode.row (bytes 20..23);
+    # node ids without a row (past n_nodes, or an allocation that failed) decode
+    # to garbage
+    base = np.array(read(lane * per + cfr_tables_bytes(node_cap, edge_cap), GAME_BYTES)).view("<u4")
+    run = np.ascontiguousarray(rec.reshape(-1, CFR_NODE_BYTES)[:, 20:24]).view("<i4")[:, 0]
+    ew = np.concatenate([np.ascontiguousarray(edges).view("<u4"), np.zeros(CFR_ROW_HDR + CFR_ROW_W, "<u4")])
+    start = np.clip(run, 0, max(0, (ew.shape[0] - CFR_ROW_HDR - CFR_ROW_W) // (CFR_EDGE_BYTES // 4)))
+    rows = np.empty((run.shape[0], CFR_ROW_W), "<u4")
+    for c in range(0, run.shape[0], 4096):                   # bounded temporaries
+        w = ew[start[c:c + 4096, None] * (CFR_EDGE_BYTES // 4) + np.arange(CFR_ROW_HDR + CFR_ROW_W)[None, :]]
         bits = np.unpackbits(np.ascontiguousarray(w[:, :CFR_ROW_MASKW]).view(np.uint8), axis=1,
                              bitorder="little")[:, :CFR_ROW_W].astype(bool)
-        rank = np.clip(np.cumsum(bits, axis=1) - 1, 0, row_cap - 1) + CFR_ROW_HDR
-        vals = np.take_along_axis(w, rank, axis=1)
-        rows = np.where(bits, vals, base[None, :]).astype("<u4").view(np.uint8)   # unused slots decode to garbage
-    edges = gather(edge_base, CFR_EB * CFR_EDGE_BYTES, ebl)
-    return nodes, edges, rows
+        rank = np.clip(np.cumsum(bits, axis=1) - 1, 0, CFR_ROW_W - 1) + CFR_ROW_HDR
+        rows[c:c + 4096] = np.where(bits, np.take_along_axis(w, rank, axis=1), base[None, :])
+    return nodes, edges, rows.view(np.uint8)

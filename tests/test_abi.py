@@ -50,18 +50,19 @@ def test_cfr_pool_layout(lib):
     assert lib.cit_cfr_pool_bytes(3, 5) % 16 == 0             # the next tree's tables 16-byte aligned
     assert lib.cit_cfr_arena_bytes(172 * 300, 172 * 300) == L.cfr_arena_bytes(172 * 300, 172 * 300) > 2 ** 38
     h.cith_cfr_arena_bytes_rows.restype = C.c_int64
-    for rc in (0, 4, 128, 368):                               # diff row slots: 16 header words + rc dwords
+    for rc in (0, 4, 128, 388):                               # diff rows: edge-slot runs, no row slots
         assert lib.cit_cfr_arena_bytes_rows(172, 17, rc) == L.cfr_arena_bytes(172, 17, rc) == \
             h.cith_cfr_arena_bytes_rows(172, 17, rc)
-    assert L.cfr_node_block_bytes(128, False) == 4096 * (72 + 576) < L.cfr_node_block_bytes(0) == \
+    assert L.cfr_node_block_bytes(128, False) == 4096 * 72 < L.cfr_node_block_bytes(0) == \
         4096 * (72 + 48 + 1552)                               # 72-B records (+ pred_node_value in pred pools)
+    assert [L.cfr_row_slots(k) for k in (0, 10, 11, 70, 388)] == [2, 2, 3, 7, 34]   # 14 header words + k, 12 a slot
     h.cith_cfr_arena_bytes_fmt.restype = C.c_int64
     for rc in (0, 128):
         for pred in (0, 1):
             assert lib.cit_cfr_arena_bytes_fmt(172, 17, rc, pred) == L.cfr_arena_bytes(172, 17, rc, bool(pred)) == \
                 h.cith_cfr_arena_bytes_fmt(172, 17, rc, pred)
     assert lib.cit_cfr_arena_bytes_fmt(1, 1, 130, 0) == -1
-    for bad in (-4, 3, 130, 372):
+    for bad in (-4, 3, 130, 392):
         assert lib.cit_cfr_arena_bytes_rows(1, 1, bad) == -1
         assert lib.cit_cfr_arena_reset_rows(None, 4, 16, 16, 1, 1, bad, None) == -1
     assert lib.cit_cfr_pool_bytes(0, 10) == -1
@@ -78,7 +79,10 @@ def test_arena_blocks():
     assert pool_bytes(2, 100, 500) == 2 * (16 + 2 * 1552) + L.cfr_arena_bytes(2, 2, 0, False)
     assert pool_bytes(2, 100, 500, pred=True) == 2 * (16 + 2 * 1552) + L.cfr_arena_bytes(2, 2)
     assert pool_bytes(2, 700_512, 2_806_144) == 2 * L.cfr_pool_bytes(700_512, 2_806_144) + \
-        L.cfr_arena_bytes(344, 344, 128, False)                # large trees: diff row slots, no pred
+        L.cfr_arena_bytes(344, 344, 388, False)                # large trees: diff rows, no pred
+    from citadels_self_play_amd.engine import pool_caps
+    assert pool_caps(200000) == (700_512, 14 * 700_512 + 4096)   # row runs in the edge cap
+    assert pool_caps(200) == (1212, 4 * 1212 + 4096)            # small trees: raw rows
 
 
 def test_bad_args_rejected(lib):

@@ -60,7 +60,7 @@ def compare_node(nodes, edges, rows, i, want, where):
 def run_cases(recs, row_cap=0):
     recs = [r for r in recs if not r.get("skip")]
     hb = HostBatch([r["seed"] for r in recs], True)
-    cf = HostCfr(hb, node_cap=8192, edge_cap=5 * 8192, row_cap=row_cap)
+    cf = HostCfr(hb, node_cap=8192, edge_cap=(16 if row_cap else 5) * 8192, row_cap=row_cap)   # rows in edge space
     cf.advance(0, 300)
     for l, r in enumerate(recs):
         assert canon.canon_game(hb.game(l)) == r["position"], r["seed"]
@@ -87,8 +87,9 @@ def run_cases(recs, row_cap=0):
                 compare_node(nodes, edges, rows, i, want, (r["seed"], k))
 
 
-# row_cap 128: node rows stored as diffs against the tree's base row (the
-# layout of large trees' pools, cit_cfr.h): same trees, rows and streams
+# row_cap 128: node rows stored as diffs against the tree's base row, runs of
+# edge slots (the layout of large trees' pools, cit_cfr.h): same trees, rows
+# and streams
 @pytest.mark.parametrize("row_cap", [0, 128])
 def test_cfr_host_train200(row_cap):
     run_cases(load_golden("cfr_train200.json.gz"), row_cap)

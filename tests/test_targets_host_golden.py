@@ -15,13 +15,13 @@ from test_targets_oracle_golden import check_targets
 
 
 @pytest.mark.parametrize("mode,row_cap", [(0, 0), (2, 0), (2, 128)])   # 2: the pruned walk (no model);
-def test_host_targets_match_reference(mode, row_cap):                    # 128: diff row slots
+def test_host_targets_match_reference(mode, row_cap):                    # 128: diff rows
     recs = load_golden("targets2000.json.gz")
     hb = HostBatch([r["seed"] for r in recs], True)
     random_position(hb, 100)
     for l, r in enumerate(recs):
         assert canon.canon_game(hb.game(l)) == r["position"], r["seed"]
-    cf = HostCfr(hb, node_cap=8192, edge_cap=8 * 8192, row_cap=row_cap, pred=row_cap == 0)   # 72-B records too
+    cf = HostCfr(hb, node_cap=8192, edge_cap=16 * 8192, row_cap=row_cap, pred=row_cap == 0)   # 72-B records too
     chosen, stats = cf.decide(2000)
     t = cfr_targets(cf, stats[:, 0], mode=mode)
     per = split_targets(t)

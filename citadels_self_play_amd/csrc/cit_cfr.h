@@ -973,6 +973,23 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   return id;
 }
 
+// n edge records from the run at src to the run at dst (runs are contiguous)
+CIT_HD void cfr_move_edges(const CfrTree& T, int dst, int src, int n) {
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(cfr_edge(T, src));
+  uint32_t* d = reinterpret_cast<uint32_t*>(cfr_edge(T, dst));
+  const int nw = n * (int)(sizeof(CfrEdge) / 4);
+#if CIT_WAVE
+  {   // up to 2 dwords per lane (n <= 8: 96 dwords), both loaded before the stores
+    static_assert(8 * sizeof(CfrEdge) / 4 <= 128, "a moved run fits two dwords per lane");
+    const int l = CFR_LANE;
+    const uint32_t a = l < nw ? s[l] : 0u, b = l + 64 < nw ? s[l + 64] : 0u;
+    if (l < nw) d[l] = a;
+    if (l + 64 < nw) d[l + 64] = b;
+  }
+#else
+  for (int i = 0; i < nw; i++) d[i] = s[i];
+#endif
+}
 CIT_HD void init_edge(CfrEdge& E, const CitOpt& o, int child) {
   E.opt = o;
   E.child = child;
@@ -1077,7 +1094,8 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n, int par, int player, int 
   }
 }
 
-CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player, int depth, int nch, int fe) {
+CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player, int depth, int nch, int fe,
+                                      int ecap) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(10);              // :153-179
   n = cfr_u(n);
@@ -1086,6 +1104,7 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player,
   depth = cfr_u(depth) + 1;
   nch = cfr_u(nch);
   fe = cfr_u(fe);
+  ecap = cfr_u(ecap);
   int pp, ps;
   cfr_parent_info(T, par, pp, ps);
   row_load(T, w_row(T, 1), n);
@@ -1113,12 +1132,18 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player,
   for (int j = 0; j < nch; j++)
     if (opt_eq((*cfr_edge(T, fe + j)).opt, key)) return;
 #endif
-  if (fe < 0) {
-    fe = alloc_edges(T, CFR_OPP_CHILDREN);
-    if (fe < 0) return;
+  if (fe < 0 || nch == ecap) {
+    // the children's edge run grows 1 -> 2 -> 4 -> 8 -> CFR_OPP_CHILDREN
+    // (most opponent nodes only ever get one child): a full run moves to a
+    // new one twice as long, the old one stays unused
+    const int ncap = fe < 0 ? 1 : (2 * ecap < CFR_OPP_CHILDREN ? 2 * ecap : CFR_OPP_CHILDREN);
+    const int nf = cfr_u(alloc_edges(T, ncap));
+    if (nf < 0) return;
+    if (fe >= 0) cfr_move_edges(T, nf, fe, nch);
     CfrNode& N = cfr_node(T, n);
-    N.first_edge = fe;
-    N.edge_cap = CFR_OPP_CHILDREN;
+    N.first_edge = nf;
+    N.edge_cap = (int16_t)ncap;
+    fe = nf;
   }
   int c = cfr_u(cfr_node(T, 1, n, depth, 0));
   if (c < 0) return;
@@ -1129,7 +1154,8 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player,
 
 CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
   CfrNode& N = cfr_node(T, n);
-  const int state = N.gs_state, nch = N.n_children, player = N.player, par = N.parent, depth = N.depth;
+  const int state = N.gs_state, nch = N.n_children, player = N.player, par = N.parent, depth = N.depth,
+            ecap = N.edge_cap;
   T.rn_node = n;
   T.rn_run = N.row;
   if (state == 0 && nch == 0) {
@@ -1138,7 +1164,7 @@ CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
   } else if (player == T.orig && nch == 0) {
     cfr_expand_own(T, n, par, player, depth);
   } else if (player != T.orig && nch < CFR_OPP_CHILDREN) {
-    cfr_expand_opponent(T, n, par, player, depth, nch, N.first_edge);
+    cfr_expand_opponent(T, n, par, player, depth, nch, N.first_edge, ecap);
   }
 }
 

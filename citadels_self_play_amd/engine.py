@@ -55,8 +55,9 @@ def node_arrays(nodes, edges, n):
 def pool_caps(iters):
     """Node / edge capacity for a cfr_train(iters) tree: measured 1.2-3.3 nodes
     per iteration (2000 iterations: up to 6,604 nodes; 200000: up to 646,897)
-    and 3.1-4.4 reserved edge slots per node, plus ROW_EDGE_SLOTS per node for
-    the diff rows of large trees (row_cap_for: ~7 slots measured); a tree that
+    and up to ~4 edge slots per node (~2 measured since opponent nodes' runs
+    grow as they fill), plus ROW_EDGE_SLOTS per node for the diff rows of
+    large trees (row_cap_for: ~7 slots measured); a tree that
     still outgrows its pool is searched again with a 4x pool
     (GameBatch._retry_overflow).  Caps bound a tree; the arena holds what the
     trees use."""

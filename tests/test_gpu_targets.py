@@ -171,7 +171,8 @@ def test_gpu_diff_rows_match_raw_rows(row_cap):
         # each node's written edge slots in node order (reserved ones never filled hold garbage)
         f, c, rp = nodes["first_edge"][:n], nodes["n_children"][:n], (nodes["flags"][:n] & 1) != 0
         idx = np.concatenate([np.arange(a, a + (40 if r else k)) for a, k, r in zip(f, c, rp) if k > 0])
-        return idx[~np.isin(idx, np.concatenate([np.arange(a + k, a + 10) for a, k, r in zip(f, c, rp) if r]))]
+        unused = [np.arange(a + k, a + 10) for a, k, r in zip(f, c, rp) if r and k > 0]   # (childless: no run)
+        return idx[~np.isin(idx, np.concatenate(unused))] if unused else idx
 
     for l, (n0, e0, r0), (n1, e1, r1) in zip((0, 7, 31), raw[6], diff[6]):
         n = int(raw[1][l, 1])

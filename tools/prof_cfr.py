@@ -76,6 +76,7 @@ def run(which=None, workloads=None):
     import torch
     import citadels_self_play_amd._lib as LL
     from citadels_self_play_amd.engine import GameBatch, pool_caps
+    which = None if which in ("", "all") else which
     loads = [("plain", LL.LIB_PATH)] + [(n, lib_of(n)) for n in VARIANTS if which in (None, n)]
     plain = {}
     for vname, path in loads:

@@ -335,22 +335,28 @@ def pmc_in_run_cfr():
     return out
 
 
-def search_roofline(pmc, alg_bytes_per_carry):
+def search_roofline(pmc, alg_bytes_per_carry, timed_ms, timed_carry):
     """The latency / issue model of a search kernel from its in-run counters
-    (totals over the child's launches, priced per carry_out): SALU floor over
-    the child's search time, wait fraction, VMEM instructions and counter
-    traffic per carry_out against SURVEY §8(d)'s algorithmic bytes."""
+    (totals over the child's launches, priced per carry_out; the child runs
+    the timed rep's seeds, unwarmed and serialised by the profiler, so its own
+    wall time is not the kernel's): SALU instructions per carry_out x the
+    timed rep's carry_outs as the SALU floor against the timed search, wait
+    fraction, VMEM instructions and counter traffic per carry_out against
+    SURVEY §8(d)'s algorithmic bytes."""
     if not pmc or "SQ_INSTS_SALU" not in pmc:
         return None
-    carry = float(pmc["carry_outs"])
-    ms = float(pmc.get("search_ms_pass2") or 0.0)            # the SQ pass's own search time
+    carry = float(pmc.get("carry_outs_pass2", pmc["carry_outs"]))    # the SQ pass's own run
     salu = pmc["SQ_INSTS_SALU"]
-    salu_floor_ms = salu / SALU_PEAK * 1e3
+    salu_timed = salu / carry * timed_carry
+    salu_floor_ms = salu_timed / SALU_PEAK * 1e3
     out = {"salu_per_carry_out": salu / carry, "valu_per_carry_out": pmc.get("SQ_INSTS_VALU", 0.0) / carry,
            "lds_per_carry_out": pmc.get("SQ_INSTS_LDS", 0.0) / carry,
            "smem_per_carry_out": pmc.get("SQ_INSTS_SMEM", 0.0) / carry,
-           "salu_floor_ms": salu_floor_ms, "search_ms": ms, "salu_frac": salu_floor_ms / ms if ms else None,
-           "salu_inst_per_s": salu / (ms * 1e-3) if ms else None, "launches": pmc.get("_launches")}
+           "salu_floor_ms": salu_floor_ms, "search_ms": timed_ms,
+           "salu_frac": salu_floor_ms / timed_ms if timed_ms else None,
+           "salu_inst_per_s": salu_timed / (timed_ms * 1e-3) if timed_ms else None,
+           "child_carry_outs": carry, "child_search_ms": float(pmc.get("search_ms_pass2") or 0.0),
+           "launches": pmc.get("_launches")}
     if pmc.get("SQ_WAVE_CYCLES"):
         out["wait_any_frac"] = pmc.get("SQ_WAIT_ANY", 0.0) / pmc["SQ_WAVE_CYCLES"]
     if "SQ_INSTS_VMEM_RD" in pmc:
@@ -695,15 +701,16 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
                     "alg_bytes": alg, "alg_bytes_per_carry_out": alg / max(1.0, carry_all), "search_ms": ms,
                     "model": "SURVEY §8(d) CFR expand bytes: 5 x CIT_GAME_BYTES per node created + 24 B per edge "
                              "slot, over the search's wall time per GPU"}
-    issue = search_roofline(pmc, alg / max(1.0, carry_all)) if pmc else None
+    issue = search_roofline(pmc, alg / max(1.0, carry_all), ms, carry_all) if pmc else None
     if issue is not None and issue.get("salu_frac") is not None:
         roof = {"bound": "latency (salu-issue floor)", "achieved": issue["salu_inst_per_s"] / 1e9,
                 "peak": SALU_PEAK / 1e9, "unit": "G SALU inst/s", "frac": issue["salu_frac"],
                 "traffic_bytes_per_carry_out": issue.get("traffic_bytes_per_carry_out"),
                 "traffic": issue.get("traffic_bytes_per_carry_out"),
-                "model": "one wave per tree runs a serial search: the SALU floor (SQ_INSTS_SALU / (256 CU x 2.4 "
-                         "GHz)) over the search time of the counter run, with its wait fraction and VMEM "
-                         "instructions per carry_out; hbm_notional keeps SURVEY §8(d)'s bytes"}
+                "model": "one wave per tree runs a serial search: the SALU floor (the counter run's "
+                         "SQ_INSTS_SALU per carry_out x the timed carry_outs / (256 CU x 2.4 GHz)) over the timed "
+                         "search, with the wait fraction and VMEM instructions per carry_out; hbm_notional keeps "
+                         "SURVEY §8(d)'s bytes"}
     else:
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -153,3 +153,28 @@ def test_gpu_config4_full_size(net, n):
         assert canon.canon_option(L.opt_from_bytes(c0[l]), g) == r["chosen"], r["seed"]
         nodes, edges, _ = b0.tree(l)
         np.testing.assert_allclose(nodes[root]["nv"], r["root"]["node_value"], rtol=0, atol=2e-6)
+
+
+def test_gpu_pred_ahead_invariant(net):
+    """cfr_pred's batched rounds (engine.PRED_AHEAD launches enqueued per host
+    poll) search exactly as a host check after every launch (PRED_AHEAD = 1):
+    decisions, stats, rows, leaf rounds and both streams are identical for 1,
+    4 (the default) and 8 rounds per poll."""
+    from citadels_self_play_amd import engine, selfplay
+    seeds = np.arange(8_100_000, 8_100_512, dtype=np.int64)
+    keep = engine.PRED_AHEAD
+    runs = []
+    try:
+        for ahead in (1, 4, 8):
+            engine.PRED_AHEAD = ahead
+            b, chosen, stats, rounds = selfplay.decide(seeds, 200, net=net)
+            torch.cuda.synchronize()
+            runs.append((chosen.cpu().numpy(), stats.cpu().numpy(), b.rows(), b.np_mt.cpu().numpy(),
+                         b.np_idx.cpu().numpy(), b.mt.cpu().numpy(), b.mt_idx.cpu().numpy(), rounds))
+    finally:
+        engine.PRED_AHEAD = keep
+    assert runs[0][7] > 10
+    for other in runs[1:]:
+        for x, y in zip(runs[0][:7], other[:7]):
+            assert np.array_equal(x, y)
+        assert other[7] == runs[0][7]

@@ -183,3 +183,35 @@ def test_gpu_diff_rows_match_raw_rows(row_cap):
         ed0, ed1 = written(n0, n), written(n1, n)
         for k in ("opt", "child", "R", "S", "CS"):           # (an edge's 4 pad bytes are never written)
             assert np.array_equal(e0[ed0][k], e1[ed1][k]), k
+
+
+@pytest.mark.parametrize("queue", [False, True])
+def test_gpu_capacity_trees_match_reference(queue):
+    """The two cfr_train(200000) trees whose card areas outgrew round 3's
+    fixed lists (seed 31000322: a museum past 16; 31007440), through the
+    config-5 product path -- simulate_games (one batch), and the tree queue
+    with one slot (each tree searched in 0.5-s slices, targets extracted after
+    its last) -- against the reference's own outputs: node and carry_out
+    counts, decision, both streams' end states, every target
+    (tests/golden/targets200000_cap.json.gz)."""
+    from citadels_self_play_amd import selfplay
+    recs = load_golden("targets200000_cap.json.gz")
+    seeds = np.array([r["seed"] for r in recs], np.int64)
+    if queue:
+        b, stats, t = selfplay.simulate_queue(seeds, 200_000, slots=1, slice_seconds=0.5)
+    else:
+        b, stats, t = selfplay.simulate_games(seeds, 200_000)
+    torch.cuda.synchronize()
+    per = _split({k: t[k] for k in ("counts", "meta", "feat", "opt_feat", "value", "dist")})
+    stats, rows, chosen = stats.cpu().numpy(), b.rows(), t["chosen"].cpu().numpy()
+    mt, idx = b.mt.cpu().numpy().view(np.uint32), b.mt_idx.cpu().numpy()
+    npmt, npidx = b.np_mt.cpu().numpy().view(np.uint32), b.np_idx.cpu().numpy()
+    for l, r in enumerate(recs):
+        root, n_nodes, n_edges, carry, err = stats[l]
+        assert err == 0, (r["seed"], hex(int(err)))
+        assert n_nodes == r["nodes"] and carry == r["carry_outs"], (r["seed"], n_nodes, carry)
+        g = L.game_from_bytes(rows[l])
+        assert canon.canon_option(L.opt_from_bytes(chosen[l]), g) == r["chosen"], r["seed"]
+        assert hash_obj(mt[:, l].tolist() + [int(idx[l])]) == r["rng_after"][0], r["seed"]
+        assert hash_obj(npmt[:, l].tolist()) == r["rng_after"][1] and int(npidx[l]) == r["rng_after"][2]
+        check_targets(per[l], r["targets"], r["seed"])

@@ -549,25 +549,26 @@ CIT_HD void row_load(CfrTree& T, uint32_t* dst, int id) {
   CFR_SYNC();
 #if CIT_WAVE
   {
-    // one round of loads: up to 4 dwords per lane from the run on (not past
+    // one round of loads: up to STG dwords per lane from the run on (not past
     // its edge block: a run never straddles one), which hold the whole row
-    // when it has at most 256 - CFR_ROW_HDR differing dwords, staged in the
-    // LDS scratch so each lane can read its dwords' values by rank; lanes
+    // when it has at most 64 * STG - CFR_ROW_HDR differing dwords, staged in
+    // the LDS scratch so each lane can read its dwords' values by rank; lanes
     // 0..12 hold the mask words, lane 13 the count; chunk j = dwords 64j..64j+63
+    constexpr int STG = CIT_SAMPLE_SCRATCH / 256 < 4 ? CIT_SAMPLE_SCRATCH / 256 : 4;
+    static_assert(STG >= 1 && 64 * STG > CFR_ROW_HDR, "row staging fits the scratch");
     const int l = CFR_LANE;
     const int left = (CFR_EB - (run & (CFR_EB - 1))) * (int)(sizeof(CfrEdge) / 4);
-    const int nw = left < 4 * 64 ? left : 4 * 64;
+    const int nw = left < STG * 64 ? left : STG * 64;
     uint32_t* stg = reinterpret_cast<uint32_t*>(cfr_ls.tmp);
-    static_assert(4 * 64 * 4 <= CIT_SAMPLE_SCRATCH, "row staging fits the scratch");
-    uint32_t v[4];
+    uint32_t v[STG];
 #pragma unroll
-    for (int q = 0; q < 4; q++) v[q] = l + 64 * q < nw ? s[l + 64 * q] : 0u;
+    for (int q = 0; q < STG; q++) v[q] = l + 64 * q < nw ? s[l + 64 * q] : 0u;
     const uint32_t mw = v[0];
     k = (uint32_t)cfr_u((int)__builtin_amdgcn_readlane((int)mw, CFR_ROW_MASKW));
     const bool staged = CFR_ROW_HDR + (int)k <= nw;
     if (staged) {
 #pragma unroll
-      for (int q = 0; q < 4; q++)
+      for (int q = 0; q < STG; q++)
         if (l + 64 * q < CFR_ROW_HDR + (int)k) stg[l + 64 * q] = v[q];
     }
     uint32_t acc = 0;

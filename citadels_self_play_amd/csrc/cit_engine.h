@@ -2189,7 +2189,13 @@ CIT_HD void kr_strip(const CitGame& g, uint16_t* kr, int role) {
   }
 }
 
-#define CIT_SAMPLE_SCRATCH 1024   // bytes of `unk` scratch cit_sample_private needs
+// bytes of `unk` scratch cit_sample_private needs (880: unknown cards [80],
+// removal counts u32[40], per-type lane masks u64[2][40]); the search also
+// stages diff rows in it (cit_cfr.h row_load: 64 dwords per 256 bytes)
+#ifndef CIT_SAMPLE_SCRATCH
+#define CIT_SAMPLE_SCRATCH 1024
+#endif
+static_assert(CIT_SAMPLE_SCRATCH >= 880 && CIT_SAMPLE_SCRATCH % 16 == 0, "determinization scratch");
 
 #if CIT_WAVE
 // Append src(i), i < cnt (<= 128), to dst[base..) skipping CIT_NO_CARD (the

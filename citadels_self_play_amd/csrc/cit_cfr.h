@@ -538,6 +538,7 @@ CIT_HD int row_run_of(const CfrTree& T, int id) {
 }
 CIT_HD uint32_t* row_run_ptr(const CfrTree& T, int run) { return reinterpret_cast<uint32_t*>(cfr_edge(T, run)); }
 CIT_HD void row_load(CfrTree& T, uint32_t* dst, int id) {
+  CIT_PROF_SCOPE(23);
   if (cfr_u(T.row_cap) == 0) {
     copy_row(T, dst, row_of(T, id));
     return;
@@ -911,6 +912,8 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   CitGame& w = cfr_w(T, which);
   uint32_t e = 0;
   int n = 0;
+  {
+  CIT_PROF_SCOPE(21);                  // skip_false_choice
   if (!cfr_u(skipped)) {
     eng_prepare(T, which);
     CfrCnt c = cfr_ucnt(eng_list_upto2(T, which));
@@ -930,6 +933,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
     e |= c.err;
     if (i > 100) done = true;
   }
+  }
   T.err |= e | w.err;
   if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_CAP; return -1; }
   int id = T.n_nodes;
@@ -940,7 +944,11 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   }
   T.n_nodes = id + 1;
   if (id == 0) row_set_base(T, w_row(T, which));   // the root: the tree's base row
-  const int run = cfr_u(row_store(T, id, w_row(T, which)));   // its row (run: diff-row pools)
+  int run;
+  {
+    CIT_PROF_SCOPE(22);
+    run = cfr_u(row_store(T, id, w_row(T, which)));   // its row (run: diff-row pools)
+  }
   CfrNode& N = cfr_node(T, id);
 #if CIT_WAVE
   {   // the header's 6 words and the 12 zero words of nv, one store per lane

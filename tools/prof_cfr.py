@@ -32,9 +32,10 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build", "cfrprof")
 NAMES = ["carry", "prepare", "list_lds", "pick", "list", "sample", "copy_row", "cfr_node", "exp_role", "exp_own",
          "exp_opp", "upd_strategy", "choose", "upd_regrets", "backprop", "live_choice",
-         "smp_used", "smp_unknown", "smp_deck", "smp_warrants", "smp_opponents"] + ["s%d" % i for i in range(21, 32)]
+         "smp_used", "smp_unknown", "smp_deck", "smp_warrants", "smp_opponents", "skip_false", "row_store",
+         "row_load"] + ["s%d" % i for i in range(24, 32)]
 VARIANTS = {"top": (8, 9, 10, 11, 12, 14, 15), "node": (5, 6, 7), "engine": (0, 1, 2, 3, 4),
-            "sample": (5, 16, 17, 18, 19, 20)}
+            "sample": (5, 16, 17, 18, 19, 20), "rows": (7, 21, 22, 23)}
 
 
 def lib_of(name):

@@ -51,7 +51,7 @@ typedef struct CitOption {
   uint64_t x;
 } CitOption;
 
-int cit_abi_version(void);              /* 6: per-player card areas (hand / just-drawn / museum share 88 slots); 5: packed value-MLP path */
+int cit_abi_version(void);              /* 7: diff rows as edge-slot runs (CfrNode.row), opponent edge runs that grow; 6: per-player card areas (hand / just-drawn / museum share 88 slots); 5: packed value-MLP path */
 int cit_game_bytes(void);              /* row width of `games` */
 int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
 int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
@@ -179,21 +179,24 @@ int cit_mlp_forward_packed(const float* feat, int M, const void* packed, float* 
  * each: int32 node-block and edge-block tables for node_cap / edge_cap,
  * padded to 16 B, then the tree's base row and a scratch row) followed by one
  * arena (cit_cfr_arena_bytes_fmt(node_blocks, edge_blocks, row_cap, pred)): a
- * 64-byte header, node blocks (CFR_NB CfrNode records of 72 B: header +
- * node_value f64[6]; with pred, CFR_NB pred_node_value f64[6]; CFR_NB row
- * slots, 16-byte aligned) and edge blocks (CFR_EB CfrEdge slots of 48 B),
- * after a ring of free block ids per kind.  A row slot holds a node's packed
- * game row raw (row_cap 0: CIT_GAME_BYTES) or as a diff against the tree's
- * base row (its root game as first created): 16 header words (a 388-bit mask
- * of the differing dwords, their count) + at most row_cap dwords (a multiple
- * of 4, <= 368); a row with more differing dwords stops the tree with
- * CIT_ERR_OVERFLOW (search it again with raw rows).  A
- * tree takes blocks as it grows (a released block first), so the arena holds
- * what the trees use, not B worst cases; a tree that reaches its own caps or
- * finds the arena exhausted stops with CIT_ERR_OVERFLOW (search it again with
- * more room).  Opponent nodes reserve 10 edges, role-pick nodes 40 slots (10
- * edges + their [6]-wide regret / strategy columns); a node's edges never
- * straddle an edge block.  Sizes are 64-bit; -1 on a bad capacity (either
+ * 64-byte header, node blocks (CFR_NB CfrNode records of 72 B: header, the
+ * row run, node_value f64[6]; with pred, CFR_NB pred_node_value f64[6]; with
+ * row_cap 0, CFR_NB raw row slots of CIT_GAME_BYTES, 16-byte aligned) and
+ * edge blocks (CFR_EB CfrEdge slots of 48 B), after a ring of free block ids
+ * per kind.  A node's game row is raw (row_cap 0) or, with row_cap > 0, a
+ * diff against the tree's base row (its root game as first created) stored
+ * as a run of ceil((14 + k) / 12) edge slots from CfrNode.row: 14 header
+ * words (a 388-bit mask of the k differing dwords, then k) and the k dwords
+ * (row_cap a multiple of 4, <= 388; a row with more than row_cap differing
+ * dwords stops the tree with CIT_ERR_OVERFLOW: search it again with raw
+ * rows).  A tree takes blocks as it grows (a released block first), so the
+ * arena holds what the trees use, not B worst cases; a tree that reaches its
+ * own caps or finds the arena exhausted stops with CIT_ERR_OVERFLOW (search it
+ * again with more room).  An own node reserves its children's edges, an
+ * opponent node a run that grows as it fills (1, 2, 4, 8, 10 slots: a full
+ * run moves to a longer one), a role-pick node 40 slots (10 edges + their
+ * [6]-wide regret / strategy columns); an edge or row run never
+ * straddles an edge block.  Sizes are 64-bit; -1 on a bad capacity (either
  * table longer than out[2] of cit_cfr_block_sizes). */
 int64_t cit_cfr_pool_bytes(int node_cap, int edge_cap);
 int64_t cit_cfr_arena_bytes_rows(int node_blocks, int edge_blocks, int row_cap);
@@ -205,7 +208,7 @@ int64_t cit_cfr_arena_bytes(int node_blocks, int edge_blocks);     /* = ..._rows
 int cit_cfr_block_sizes(int32_t* out);
 /* Before a search (cit_cfr_decide, or the first cit_cfr_pred_step): every
  * table entry -1 and the arena empty with node_blocks / edge_blocks capacity
- * and row slots of row_cap.  pool must hold B * cit_cfr_pool_bytes +
+ * and rows of format row_cap.  pool must hold B * cit_cfr_pool_bytes +
  * cit_cfr_arena_bytes_rows(...) bytes.  cit_cfr_arena_reset = row_cap 0. */
 int cit_cfr_arena_reset_rows(void* pool, int B, int node_cap, int edge_cap, int node_blocks, int edge_blocks,
                              int row_cap, hipStream_t stream);
@@ -220,7 +223,7 @@ int cit_cfr_arena_reset(void* pool, int B, int node_cap, int edge_cap, int node_
 int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */
 /* Error bits of a search (stats[5*l+4]) beside the engine's CIT_ERR_* bits:
  * with CIT_ERR_OVERFLOW (0x1), which node-pool capacity ran out -- 0x1000 the
- * shared arena, 0x2000 the tree's node / edge caps, 0x4000 a diff row slot.
+ * shared arena, 0x2000 the tree's node / edge caps (rows included), 0x4000 a diff row past row_cap.
  * Only these are worth a second search (with more room / raw rows); an
  * overflow without them is an engine list capacity (e.g. a museum of more
  * than 16 cards) that no retry fixes. */

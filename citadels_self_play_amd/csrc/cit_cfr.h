@@ -441,18 +441,35 @@ CIT_HD uint32_t* w_row(const CfrTree& T, int which) { return reinterpret_cast<ui
 #define CIT_NOINLINE inline
 #endif
 
+// The search's two streams sit in its LDS block (CfrTree::py / np, device);
+// an engine call or a numpy draw works on a register copy of the stream's
+// state (word pointer, position, register window) and hands it back once,
+// so no draw reads and writes the position through LDS.
+template <class F>
+CIT_HD auto cfr_with_np(CfrTree& T, F f) {
+  CitMT r = T.np;
+  auto v = f(r);
+  T.np = r;
+  return v;
+}
+
 // option.carry_out on working row `which`, counted; returns the winner (-1: none)
 CIT_NOINLINE int eng_carry(CfrTree& T_in, int which, CitOpt o_in) {
   CIT_PROF_SCOPE(0);
   CfrTree& T = CFR_T(T_in);
   CitOpt o = cfr_uopt(o_in);
   T.carry_outs++;
-  return cit_carry_out(cfr_w(T, cfr_u(which)), o, T.py);
+  CitMT py = T.py;               // (a register copy for the call: see cfr_with_np)
+  const int w = cit_carry_out(cfr_w(T, cfr_u(which)), o, py);
+  T.py = py;
+  return w;
 }
 CIT_NOINLINE void eng_prepare(CfrTree& T_in, int which) {
   CIT_PROF_SCOPE(1);
   CfrTree& T = CFR_T(T_in);
-  cit_prepare_options(cfr_w(T, cfr_u(which)), T.py, cfr_glb(T.seer));
+  CitMT py = T.py;
+  cit_prepare_options(cfr_w(T, cfr_u(which)), py, cfr_glb(T.seer));
+  T.py = py;
 }
 CIT_NOINLINE CitOpt eng_pick(CfrTree& T_in, int which, int k) {
   CIT_PROF_SCOPE(3);
@@ -498,7 +515,9 @@ CIT_NOINLINE CfrCnt eng_list_upto2(CfrTree& T_in, int which) {
 CIT_NOINLINE void eng_sample(CfrTree& T_in, int which, int orig, int role_sample) {
   CIT_PROF_SCOPE(5);
   CfrTree& T = CFR_T(T_in);
-  cit_sample_private(cfr_w(T, cfr_u(which)), cfr_u(orig), cfr_u(role_sample) != 0, T.py, cfr_tmp(T));
+  CitMT py = T.py;
+  cit_sample_private(cfr_w(T, cfr_u(which)), cfr_u(orig), cfr_u(role_sample) != 0, py, cfr_tmp(T));
+  T.py = py;
 }
 
 // deepcopy(game): the team copies one row (inlined, so each call site's
@@ -1035,15 +1054,18 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n, int depth) {
   cfr_node(T, n).first_edge = f;
   cfr_node(T, n).edge_cap = CFR_ROLE_CHILDREN;
   CitGame& h = cfr_w(T, 1);
+  // the node's row once into working row 0 (free during an expansion), then
+  // an LDS copy per child instead of a pool read behind the last child's stores
+  row_load(T, w_row(T, 0), n);
   for (int r = 0; r < CFR_ROLE_CHILDREN && !T.err; r++) {
-    row_load(T, w_row(T, 1), n);
+    copy_row(T, w_row(T, 1), w_row(T, 0));
     CitOpt last = mk(O_NUM_NAMES, 0);
     int guard = 0;
     while (h.gs_state != 1 && !T.err) {
       eng_prepare(T, 1);
       CfrCnt c = cfr_ucnt(eng_list_lds(T, 1));
       T.err |= c.err;
-      int k = np_choice_uniform(T.np, c.n, T.err);
+      int k = cfr_with_np(T, [&](CitMT& r_) { return np_choice_uniform(r_, c.n, T.err); });
       if (T.err) break;
       last = k < CFR_LBUF ? cfr_uopt(cfr_lbuf(T)[k]) : cfr_uopt(eng_pick(T, 1, k));
       eng_carry(T, 1, last);
@@ -1087,8 +1109,35 @@ CIT_NOINLINE void cfr_expand_own(CfrTree& T_in, int n, int par, int player, int 
   N.edge_cap = (int16_t)cnt;
   const CitOpt* ob = cfr_glb(T.optbuf);
   CitGame& h = cfr_w(T, 1);
+#if CIT_WAVE
+  // the first 64 options in registers (lane j: option j), one round of loads:
+  // a load per child would wait behind the previous child's stores (gfx9's
+  // vmcnt counts both)
+  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+  {
+    const int l = CFR_LANE;
+    if (l < cnt) {
+      const uint4 v = *reinterpret_cast<const uint4*>(ob + l);
+      q0 = v.x;
+      q1 = v.y;
+      q2 = v.z;
+      q3 = v.w;
+    }
+  }
+#endif
   for (int i = 0; i < cnt && !T.err; i++) {
-    CitOpt o = ob[i];
+    CitOpt o;
+#if CIT_WAVE
+    if (i < 64) {
+      uint32_t w4[4] = {(uint32_t)__builtin_amdgcn_readlane((int)q0, i), (uint32_t)__builtin_amdgcn_readlane((int)q1, i),
+                        (uint32_t)__builtin_amdgcn_readlane((int)q2, i), (uint32_t)__builtin_amdgcn_readlane((int)q3, i)};
+      __builtin_memcpy(&o, w4, 16);
+    } else {
+      o = ob[i];
+    }
+#else
+    o = ob[i];
+#endif
     copy_row(T, w_row(T, 1), w_row(T, 0));
     if (sample) eng_sample(T, 1, T.orig, role_sample);
     opt_mutate(o, h);
@@ -1122,7 +1171,7 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player,
   eng_prepare(T, 1);
   CfrCnt lc = cfr_ucnt(eng_list_lds(T, 1));
   T.err |= lc.err | h.err;
-  int k = np_choice_uniform(T.np, lc.n, T.err);
+  int k = cfr_with_np(T, [&](CitMT& r_) { return np_choice_uniform(r_, lc.n, T.err); });
   if (T.err) return;
   CitOpt o = k < CFR_LBUF ? cfr_uopt(cfr_lbuf(T)[k]) : cfr_uopt(eng_pick(T, 1, k));
   opt_mutate(o, h);
@@ -1311,11 +1360,11 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
     if (cfr_ls.cnode == n && cfr_ls.cnch == nch) {   // update_strategy(n) left CS in LDS
       const double* cb = cfr_ls.cbuf;
       double tot = np_sum([cb](int i) { return cb[i]; }, nch, T.err);
-      return np_choice(T.np, [cb, tot](int i) { return cb[i] / tot; }, nch, T.err);
+      return cfr_with_np(T, [&](CitMT& r_) { return np_choice(r_, [cb, tot](int i) { return cb[i] / tot; }, nch, T.err); });
     }
 #endif
     double tot = np_sum([E](int i) { return E[i].CS; }, nch, T.err);
-    return np_choice(T.np, [E, tot](int i) { return E[i].CS / tot; }, nch, T.err);
+    return cfr_with_np(T, [&](CitMT& r_) { return np_choice(r_, [E, tot](int i) { return E[i].CS / tot; }, nch, T.err); });
   }
   const CfrWide* W = cfr_wide(T, fe);
   // weighted_average_strategy (:51-65) over turn_orders_for_roles of the node's game
@@ -1330,8 +1379,8 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
     w[a] = acc / (double)hs;
   }
   double s = np_sum([&w](int i) { return w[i < CFR_ROLE_CHILDREN ? i : 0]; }, nch, T.err);
-  if (s == 0.0) return np_choice_uniform(T.np, nch, T.err);
-  return np_choice(T.np, [&w, s](int i) { return w[i] / s; }, nch, T.err);
+  if (s == 0.0) return cfr_with_np(T, [&](CitMT& r_) { return np_choice_uniform(r_, nch, T.err); });
+  return cfr_with_np(T, [&](CitMT& r_) { return np_choice(r_, [&w, s](int i) { return w[i] / s; }, nch, T.err); });
 }
 
 // ------------------------------------------------------------- backup
@@ -1536,7 +1585,7 @@ CIT_NOINLINE CitOpt cfr_live_choice(CfrTree& T_in, int root) {
   const CitOpt* ob = cfr_glb(T.optbuf);
   double sum = 0.0;
   for (int j = 0; j < nl; j++) sum += W[ob[j].a].S[pid];
-  int j = np_choice(T.np, [&](int i) { return W[ob[i].a].S[pid] / sum; }, nl, T.err);
+  int j = cfr_with_np(T, [&](CitMT& r_) { return np_choice(r_, [&](int i) { return W[ob[i].a].S[pid] / sum; }, nl, T.err); });
   row_restore(T, root, w_row(T, 0));
   if (T.err || j < 0) return mk(O_NUM_NAMES, 0);
   return ob[j];

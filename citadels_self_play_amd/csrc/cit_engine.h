@@ -311,9 +311,31 @@ CIT_HD int deck_take_like(CitGame& g, int c) {
 // window (a readlane each instead of an LDS round trip per draw); the swaps
 // stay serial (LDS operations of one wave are in order, so a swap's reads
 // never wait on the previous swap's writes).
+#ifndef CIT_SHUFFLE_REG
+#define CIT_SHUFFLE_REG 0
+#endif
 template <class At>
 CIT_HD void shuffle_seq(CitMT& rng, int n, At at) {
 #if CIT_WAVE
+  if (CIT_SHUFFLE_REG && rng.coop && n > 1 && n <= 128) {
+    // the sequence in two VGPRs (lane l: elements l and 64 + l); a swap is
+    // two readlanes at wave-uniform indices and two lane selects, the same
+    // draws in the same order, one load and one store of the sequence
+    CitMT w = cit_mt_window(rng);
+    const int l = cit_lane();
+    int v0 = l < n ? (int)at(l) : 0, v1 = l + 64 < n ? (int)at(l + 64) : 0;
+    for (int i = n - 1; i > 0; i--) {
+      const int j = __builtin_amdgcn_readfirstlane((int)mt_randbelow(w, (uint32_t)(i + 1)));
+      const int x = i < 64 ? __builtin_amdgcn_readlane(v0, i) : __builtin_amdgcn_readlane(v1, i - 64);
+      const int y = j < 64 ? __builtin_amdgcn_readlane(v0, j) : __builtin_amdgcn_readlane(v1, j - 64);
+      v0 = l == i ? y : (l == j ? x : v0);
+      v1 = l + 64 == i ? y : (l + 64 == j ? x : v1);
+    }
+    if (l < n) at(l) = (uint8_t)v0;
+    if (l + 64 < n) at(l + 64) = (uint8_t)v1;
+    cit_mt_unwindow(rng, w);
+    return;
+  }
   if (rng.coop && n > 1) {
     CitMT w = cit_mt_window(rng);
     for (int i = n - 1; i > 0; i--) {

@@ -10,6 +10,12 @@
 // sweeps.
 #include <hip/hip_runtime.h>
 
+// random.shuffle over a sequence of up to 128 in two VGPRs (cit_engine.h
+// shuffle_seq): the rollout's one batch 0.92 -> 0.94 G, the overlapped
+// headline unchanged (profiles/r04/rollout_waves/summary_shuffle.txt); the
+// search unit keeps the LDS swaps (8 % slower there: its registers are full)
+#define CIT_SHUFFLE_REG 1
+
 #include "../../include/citadels.h"
 #include "cit_area_test.h"
 #include "cit_engine.h"

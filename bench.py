@@ -409,7 +409,7 @@ def _reduce(vals, world, dev, maxes=()):
 def run_rollout(args, world, rank, dev, n_dev, pmc):
     """Config 2: the headline.  Returns the bench line (rank 0) or None."""
     from citadels_self_play_amd import layout as L
-    from citadels_self_play_amd.engine import GameBatch
+    from citadels_self_play_amd.engine import GameBatch, side_streams
 
     B, K, W, S = args.batch, args.steps, args.warmup, max(1, args.streams)
     seer = None
@@ -431,7 +431,7 @@ def run_rollout(args, world, rank, dev, n_dev, pmc):
     # batch k goes to stream k % S, so the next batches' games take the SIMD
     # slots the finished games of earlier batches leave (the launch tail).
     stream = torch.cuda.current_stream()
-    streams = [stream] if S == 1 else [torch.cuda.Stream(device=dev) for _ in range(S)]
+    streams = [stream] if S == 1 else side_streams(dev, S)     # (one pool for every leg: engine.side_streams)
     if S > 1:
         # A stream's first launches set up its hardware queue: warm every stream
         # with a small init + rollout of its own (untimed, seeds outside the timed ones).
@@ -750,7 +750,7 @@ def _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap):
     slots the finished trees of earlier batches free (a launch lasts as long
     as its longest tree).  Decisions of all ranks / max-over-ranks time."""
     from citadels_self_play_amd import selfplay
-    from citadels_self_play_amd.engine import ERR_OVERFLOW, GameBatch
+    from citadels_self_play_amd.engine import ERR_OVERFLOW, GameBatch, side_streams
     K, S = args.cfr_stream_batches, args.cfr_streams
     batches = []
     for k in range(K + S):
@@ -761,7 +761,7 @@ def _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap):
         b._pool(node_cap, 5 * node_cap)
         batches.append(b)
     torch.cuda.synchronize()
-    sts = [torch.cuda.Stream(device=dev) for _ in range(S)]
+    sts = side_streams(dev, S)
     for i, st in enumerate(sts):                       # warm each stream's queue (untimed batches)
         with torch.cuda.stream(st):
             batches[K + i]._cfr_decide(iters, node_cap, 5 * node_cap)

@@ -91,12 +91,18 @@ _side_streams = {}
 
 
 def side_streams(device, n):
-    """n HIP streams of `device` kept for reuse (a stream's first launches set up
-    its hardware queue: fresh streams per call would pay that every time)."""
-    key = (str(device), n)
-    if key not in _side_streams:
-        _side_streams[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
-    return _side_streams[key]
+    """The first n of one pool of HIP streams per device, shared by every
+    caller (the bench's stream legs, cfr_pred's groups, the tree queue): a
+    stream's first launches set up its hardware queue, and a process gets 4
+    of them (GPU_MAX_HW_QUEUES on the box), so streams past that share a
+    queue and serialise -- fresh streams per leg would leave later legs'
+    streams on shared queues."""
+    pool = _side_streams.setdefault(str(device), [])
+    while len(pool) < n:
+        pool.append(torch.cuda.Stream(device=device))
+    return pool[:n]
+
+
 ROW_CAP_MIN_BLOCKS = 16
 
 

@@ -325,8 +325,9 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     parts, nxt, n_slices, n_done = [], S, 0, 0
     ticks = max(1, int(slice_seconds * 1e8))
     ran = np.zeros(S, bool)
-    main, side = torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev)
-    rstream = torch.cuda.Stream(device=dev)
+    from .engine import side_streams
+    main = torch.cuda.current_stream(dev)
+    side, rstream = side_streams(dev, 2)
     early = []            # overflowed trees searched again at once, beside the queue: (queue ids, batch, chosen, stats)
     requeue, retries = [], {}
     pending = None        # (slots, queue ids) finished last slice: targets extracted during this slice

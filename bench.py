@@ -631,6 +631,7 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
     from citadels_self_play_amd import selfplay
     from citadels_self_play_amd.engine import GameBatch, pool_caps
     iters = {3: 200, 4: 200, 5: args.cfg5_iters}[config]
+    shard_leg = per_gpu is not None
     if per_gpu is None:
         per_gpu = {3: 1024, 4: max(1, 4096 // world), 5: args.cfg5_trees}[config]
     net = _value_net(dev) if config == 4 else None
@@ -688,6 +689,9 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
     streams = None
     if config == 3 and args.cfr_streams > 1:
         streams = _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap)
+    rounds = None
+    if config == 5 and args.cfg5_rounds > 1 and warm_rep and not shard_leg:
+        rounds = _cfg5_rounds(args, world, rank, dev, iters, per_gpu)
     if rank != 0:
         return None
     med = sorted(reps, key=lambda r: r["value"])[len(reps) // 2]
@@ -726,7 +730,7 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
            "get_all_targets(200), tree queue, targets all-gathered" % (per_gpu, iters)}[config],
         "per_gpu": per_gpu,
         "value": streams["value"] if streams else med["value"], "unit": "trees/s" if config == 5 else "decisions/s",
-        "value_one_batch": med["value"], "streams": streams,
+        "value_one_batch": med["value"], "streams": streams, "rounds": rounds,
         "carry_out_per_s": med["carry_out_per_s"], "reps": len(reps), "median": med,
         "all_reps_value": [r["value"] for r in reps],
         "roofline": roof}
@@ -784,6 +788,49 @@ def _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap):
                     "value_one_batch is the median of one batch at a time"}
 
 
+def _cfg5_rounds(args, world, rank, dev, iters, per_gpu):
+    """Config 5 as train_from_scratch generates it, round after round:
+    `--cfg5-rounds` rounds of `per_gpu` trees per GPU through ONE
+    selfplay.TreeQueue, every round added up front, so round r + 1's trees
+    search in the slots (and arena blocks) round r's finished trees free
+    while its longest trees run on; each round's targets are all-gathered
+    when it completes.  `value` = all trees / the whole run; `steady_state` =
+    trees per round / the mean time between consecutive rounds' completions
+    (the rate once the queue is full, the first round's ramp excluded)."""
+    from citadels_self_play_amd import selfplay
+    R = args.cfg5_rounds
+    torch.cuda.synchronize()
+    _barrier(world)
+    t0 = time.perf_counter()
+    q = selfplay.TreeQueue(iters, per_gpu)
+    for r in range(R):
+        q.add(selfplay.shard(per_gpu * world, base_seed=CFR_SEED + (90 + r) * 1_000_000))
+    n_targets, errs, carry = 0, 0, 0.0
+    for r in range(R):
+        q.run(r)
+        _, stats, t = q.result(r)
+        f, v = selfplay.all_gather_targets(t["feat"], t["value"])
+        n_targets += int(f.shape[0])
+        errs += int((stats[:, 4] != 0).sum())
+        carry += float(stats[:, 3].double().sum())
+    done = [q.rounds[r].t_done - t0 for r in range(R)]
+    S, oc = q.S, q.overcommit
+    q.close()
+    torch.cuda.synchronize()
+    _barrier(world)
+    el = time.perf_counter() - t0
+    el, trees, carry, errs, *done = _reduce([el, per_gpu * world * R, carry, errs] + done, world, dev,
+                                            maxes=tuple(range(0, 1)) + tuple(range(4, 4 + R)))
+    gaps = np.diff(done)
+    return {"value": trees / el, "unit": "trees/s", "rounds": R, "trees_per_round": per_gpu * world,
+            "seconds": el, "round_done_s": done, "steady_state": per_gpu * world / float(np.mean(gaps)),
+            "first_round_s": done[0], "carry_out_per_s": carry / el, "error_lanes": int(errs),
+            "pooled_targets": n_targets, "slots": S, "overcommit": oc,
+            "note": "rounds of trees through one TreeQueue, all added up front (the next round's trees take the "
+                    "slots the current round's tail frees); steady_state = trees per round / mean gap between "
+                    "round completions"}
+
+
 def _cpu_model():
     from citadels_self_play_amd import models
     torch.manual_seed(0)
@@ -819,6 +866,8 @@ def main():
     ap.add_argument("--cfr-stream-batches", type=int, default=8, help="config 3: batches in the streams run")
     ap.add_argument("--cfg5-trees", type=int, default=1920, help="config 5 trees per GPU")
     ap.add_argument("--cfg5-iters", type=int, default=200000, help="config 5 cfr_train iterations per tree")
+    ap.add_argument("--cfg5-rounds", type=int, default=3,
+                    help="config 5: data rounds through one cross-round tree queue (the `rounds` figure; 1 = off)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the real path); gloo only to rehearse N>1 ranks on one GPU")
     args = ap.parse_args()

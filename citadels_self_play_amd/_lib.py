@@ -38,6 +38,9 @@ _SIGS = {
     "cit_mlp_pack": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "cit_mlp_work_bytes": ([i32], u64),
     "cit_mlp_forward_packed": ([vp, i32, vp, vp, vp, vp, u64, vp], i32),
+    "cit_mlp_wave_bytes": ([], u64),
+    "cit_mlp_pack_wave": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    "cit_mlp_forward_wave": ([vp, i32, vp, vp, vp, vp], i32),
     "cit_cfr_pool_bytes": ([i32, i32], i64),
     "cit_cfr_arena_bytes": ([i32, i32], i64),
     "cit_cfr_block_sizes": ([vp], i32),
@@ -67,6 +70,8 @@ _SIGS = {
                            vp], i32),
     "cit_cfr_pred_slice": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, i64,
                             vp, vp, vp], i32),
+    "cit_cfr_pred_fused": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp,
+                            vp], i32),
 }
 
 

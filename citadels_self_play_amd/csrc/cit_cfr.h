@@ -23,6 +23,7 @@
 #include <math.h>
 
 #include "cit_engine.h"
+#include "cit_mlp_wave.h"
 
 #define CFR_OPP_CHILDREN 10
 #define CFR_ROLE_CHILDREN 10
@@ -1630,13 +1631,55 @@ CIT_NOINLINE void cfr_write_feat(CfrTree& T_in, int n, float* feat) {
   CFR_SYNC();
 }
 
+#if CIT_WAVE
+// The leaf evaluation inside the search kernel (cit_cfr_pred_fused): node n's
+// encode_game row (player 5 for a role-pick node, as cfr_write_feat) straight
+// into LDS and the single-row forward of cit_mlp_wave.h over it.  Its scratch
+// (MLPW_R_FLOATS floats) overlays the working rows w0 / w1, the list buffer
+// and the strategy copies: none of them carries anything across a leaf
+// evaluation (a suspended tree resumes in a fresh launch with none of them),
+// except the normalised CS of node cnode, which is dropped.  The
+// probabilities end at cfr_mlp_lds() + MLPW_R_PROBS.
+__device__ __forceinline__ mlpw_lds_t* cfr_mlp_lds() { return (mlpw_lds_t*)(&cfr_ls.w[0][0]); }
+static_assert(offsetof(CfrLds, lbuf) == offsetof(CfrLds, w) + sizeof(((CfrLds*)0)->w) &&
+                  offsetof(CfrLds, sbuf) == offsetof(CfrLds, lbuf) + sizeof(((CfrLds*)0)->lbuf) &&
+                  offsetof(CfrLds, cbuf) == offsetof(CfrLds, sbuf) + sizeof(((CfrLds*)0)->sbuf) &&
+                  offsetof(CfrLds, cbuf) + sizeof(((CfrLds*)0)->cbuf) - offsetof(CfrLds, w) >= 4 * MLPW_R_FLOATS,
+              "the leaf evaluation's LDS scratch overlays w, lbuf, sbuf and cbuf");
+static_assert(4 * MLPW_R_X >= CIT_GAME_BYTES, "a diff row loaded into w0 stays clear of the encoded row");
+CIT_NOINLINE void cfr_leaf_eval(CfrTree& T_in, int n, const float* wave_w) {
+  CIT_PROF_SCOPE(24);
+  CfrTree& T = CFR_T(T_in);
+  n = cfr_u(n);
+  int pid = (cfr_node(T, n).flags & NF_ROLE_PICK) ? 5 : -1;
+  mlpw_lds_t* R = cfr_mlp_lds();
+  CFR_SYNC();
+  for (int i = CFR_LANE; i < MLPW_IN + 2; i += CFR_TEAM) R[MLPW_R_X + i] = 0.0f;
+  CFR_SYNC();
+  float* x = (float*)(R + MLPW_R_X);
+  if (cfr_u(T.row_cap) == 0) {
+    cit_encode_game<float, false>(*reinterpret_cast<const CitGame*>(row_of(T, n)), x, pid);
+  } else {
+    row_load(T, w_row(T, 0), n);
+    CFR_SYNC();
+    cit_encode_game<float, false>(cfr_w(T, 0), x, pid);
+  }
+  mlpw_forward(wave_w, R);
+  cfr_ls.cnode = -1;
+}
+#endif
+
 // One resumption.  Working row 0 must hold the lane's game when S.phase ==
 // CP_INIT.  Returns 1 when suspended for an evaluation, 2 when `bud` ran out
 // at an iteration boundary (S.phase stays CP_RUN: the next resumption goes
 // on from S.cur / S.it exactly where this one stopped), 0 when done (S.phase
-// == CP_DONE).
+// == CP_DONE).  With `wave_w` (device; the wave-layout weights of
+// cit_mlp_pack_wave) a leaf is evaluated in place (cfr_leaf_eval) and the
+// tree never suspends: the same tree as suspending, the MLP being bitwise the
+// same.
 CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_depth, const float* probs_in,
-                              float* feat, CitOpt& chosen, bool root_skipped = false, CfrBudget* bud = nullptr) {
+                              float* feat, CitOpt& chosen, bool root_skipped = false, CfrBudget* bud = nullptr,
+                              const float* wave_w = nullptr) {
   CfrTree& T = CFR_T(T_in);
   CfrState& S = CFR_S(S_in);
   iters = cfr_u(iters);
@@ -1645,6 +1688,13 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
   if (S.phase == CP_DONE) return 0;
   if (S.phase == CP_INIT) {
     S.orig = T.orig;
+    if (!T.arena->pred) {          // pred_node_value needs the pool's side arrays (cit_cfr_arena_reset_fmt pred=1)
+      T.err |= CIT_ERR_UNSUPPORTED;
+      S.root = -1;
+      S.phase = CP_DONE;
+      chosen = mk(O_NUM_NAMES, 0);
+      return 0;
+    }
     int root = cfr_u(cfr_node(T, 0, -1, 0, root_skipped ? 1 : 0));
     S.root = root;
     S.it = 0;
@@ -1681,10 +1731,21 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
       cfr_expand(T, n);
       if (T.err) break;
       if (!(cfr_node(T, n).flags & NF_PRED)) {
-        cfr_write_feat(T, n, feat);
-        S.pending = n;
-        S.phase = CP_WAIT;
-        return 1;
+#if CIT_WAVE
+        if (wave_w) {                    // evaluate in place (cit_cfr_pred_fused)
+          cfr_leaf_eval(T, n, wave_w);
+          const mlpw_lds_t* pr = cfr_mlp_lds() + MLPW_R_PROBS;
+          double* pred = cfr_pred_of(T, n);
+          for (int k = 0; k < 6; k++) pred[k] = (double)(5.0f * pr[k]);   // as the CP_WAIT resumption
+          cfr_node(T, n).flags |= NF_PRED;
+        } else
+#endif
+        {
+          cfr_write_feat(T, n, feat);
+          S.pending = n;
+          S.phase = CP_WAIT;
+          return 1;
+        }
       }
       cfr_backprop_arr(T, n, cfr_pred_of(T, n), true);
       cfr_update_strategy(T, n);

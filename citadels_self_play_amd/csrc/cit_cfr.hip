@@ -211,6 +211,70 @@ __global__ __launch_bounds__(64) CFR_OCC void k_cfr_pred_step(uint32_t* games, u
   }
 }
 
+// cfr_pred + the live choice per tree in ONE launch (cit_cfr_pred_fused):
+// leaves are evaluated inside the kernel (cfr_leaf_eval: the single-row MLP
+// over the wave-layout weights), so no tree waits for another tree's leaf or
+// for a host round; outputs as k_cfr_decide, plus the final CfrState.
+__global__ __launch_bounds__(64) CFR_OCC void k_cfr_pred_fused(uint32_t* games, uint32_t* mt, uint32_t* idx, uint32_t* npmt,
+                                                       uint32_t* npidx, uint64_t* seer, int B, int iters, int flags,
+                                                       const int32_t* orig, int max_depth, uint8_t* pool, int node_cap,
+                                                       int edge_cap, CitOpt* optbuf, const float* wave_w,
+                                                       CfrState* state, CitOpt* chosen, int32_t* stats, int base_off) {
+  long l = blockIdx.x;
+  if (l >= B) return;
+#ifdef CFR_TREE_CLOCK
+  unsigned long long tc0 = wall_clock64();
+#endif
+  cfr_prof_reset();
+  CfrState& S = cfr_ls.S;
+  S = CfrState{};           // CP_INIT (every lane stores the same value)
+  CfrTree& T = cfr_ls.T;
+  if (!tree_setup(mt, idx, npmt, npidx, seer, B, l, pool, node_cap, edge_cap, optbuf, flags, base_off)) {
+    if (threadIdx.x == 0) {
+      S.err = (int)CIT_ERR_UNSUPPORTED;
+      S.root = -1;
+      S.phase = CP_DONE;
+      if (state) state[l] = S;
+      chosen[l] = mk(O_NUM_NAMES, 0);
+      stats[5 * l + 0] = -1;
+      stats[5 * l + 1] = stats[5 * l + 2] = stats[5 * l + 3] = 0;
+      stats[5 * l + 4] = (int)CIT_ERR_UNSUPPORTED;
+    }
+    return;
+  }
+  T.n_nodes = T.n_edges = 0;
+  T.err = 0;
+  T.carry_outs = 0;
+  copy_row(T, cfr_ls.w[0], games + l * ROW_W);
+  T.orig = orig ? orig[l] : cfr_w(T, 0).gs_pid;
+  CitOpt c;
+  cfr_pred_run(T, S, iters, max_depth, nullptr, nullptr, c, (flags & CIT_CFR_ROOT_SKIPPED) != 0, nullptr, wave_w);
+  cfr_state_save(T, S);
+  int root = cfr_u(S.root);
+  if (root >= 0) row_load(T, games + l * ROW_W, root);
+  tables_store(T);
+  mt_stage_out(cfr_ls.py, mt, B, l);
+  mt_stage_out(cfr_ls.np, npmt, B, l);
+  if (threadIdx.x == 0) {
+    if (state) state[l] = S;
+    chosen[l] = c;
+    idx[l] = T.py.pos;
+    npidx[l] = T.np.pos;
+    stats[5 * l + 0] = root;
+    stats[5 * l + 1] = T.n_nodes;
+    stats[5 * l + 2] = T.n_edges;
+    stats[5 * l + 3] = (int)T.carry_outs;
+    stats[5 * l + 4] = (int)T.err;
+#ifdef CFR_TREE_CLOCK
+    if (l < 65536) {
+      g_tree_clock[2 * l] = tc0;
+      g_tree_clock[2 * l + 1] = wall_clock64();
+    }
+#endif
+  }
+  cfr_prof_flush();
+}
+
 // One slice of cfr_train per tree (the tree queue of simulate_games): the
 // tree resumes from its CfrState and runs until `ticks` of the wall clock
 // have passed (then lane 0 adds 1 to *running) or it is done (then as
@@ -477,6 +541,21 @@ int cit_cfr_pred_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np
                      (uint32_t*)games, mt, mt_idx, np_mt, np_idx, seer, B, iters, flags, orig_player, max_depth,
                      (uint8_t*)pool, node_cap, edge_cap, (CitOpt*)optbuf, (CfrState*)state, probs, feat,
                      (CitOpt*)chosen, waiting, (uint64_t)slice_ticks, running, d.base_off);
+  CHECK_LAUNCH();
+}
+
+int cit_cfr_pred_fused(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                       int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,
+                       int node_cap, int edge_cap, CitOption* optbuf, const void* wave_weights, void* state,
+                       CitOption* chosen, int32_t* stats, hipStream_t stream) {
+  if (B <= 0 || iters < 0 || cit_cfr_pool_bytes(node_cap, edge_cap) < 0 || !games || !mt || !mt_idx || !np_mt ||
+      !np_idx || !seer || !pool || !optbuf || !wave_weights || !chosen || !stats)
+    return -1;
+  DynLds d = dyn_lds(pool, node_cap, edge_cap);
+  hipLaunchKernelGGL(k_cfr_pred_fused, dim3(B), dim3(64), d.bytes, stream, (uint32_t*)games, mt, mt_idx, np_mt,
+                     np_idx, seer, B, iters, flags, orig_player, max_depth, (uint8_t*)pool, node_cap, edge_cap,
+                     (CitOpt*)optbuf, (const float*)wave_weights, (CfrState*)state, (CitOpt*)chosen, stats,
+                     d.base_off);
   CHECK_LAUNCH();
 }
 

@@ -2585,9 +2585,11 @@ CIT_HD void cit_sample_private(CitGame& g, int orig, bool role_sample, CitMT& rn
 #define CIT_OPT_FEAT 131
 // Game.encode_game (game.py:91-128), written as 418 floats into `out`.
 // pid >= 0 replaces gamestate.player_id (expand_role_pick does that, :120-123).
-template <class F>
+// zero = false: `out` is already zeroed.
+template <class F, bool zero = true>
 CIT_HD void cit_encode_game(const CitGame& g, F* out, int pid = -1) {
-  for (int i = 0; i < CIT_FEAT; i++) out[i] = 0;
+  if (zero)
+    for (int i = 0; i < CIT_FEAT; i++) out[i] = 0;
   int cur = pid >= 0 ? pid : g.gs_pid;
   for (int r = 0; r < 8; r++) out[r * 3 + g.roles[r] % 3] = 1;                 // [8,3] role variants
   for (int p = 0; p < CIT_NP; p++) {                                              // [6,8] confirmed roles

@@ -473,7 +473,7 @@ int cit_roll_clock_read(unsigned long long* out, int n) {
 }
 #endif
 
-int cit_abi_version(void) { return 7; }
+int cit_abi_version(void) { return 8; }
 int cit_game_bytes(void) { return CIT_GAME_BYTES; }
 int cit_seer_scratch_words(void) { return CIT_SEER_MAX; }
 

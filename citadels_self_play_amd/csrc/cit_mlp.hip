@@ -23,6 +23,7 @@
 
 #include "../../include/citadels.h"
 #include "cit_engine.h"
+#include "cit_mlp_wave.h"
 
 #define MLP_IN 418
 #define MLP_H1 512
@@ -365,6 +366,45 @@ __global__ void k_encode_options(const uint32_t* __restrict__ games, const CitOp
   cit_encode_option(opts[i], g, out + i * CIT_OPT_FEAT);
 }
 
+// ------------------------------------------------------- one row per wave
+// The wave layout (cit_mlp_wave.h) of the folded weights, and the single-row
+// forward the search runs inside its kernel (cit_cfr_pred_fused), here one
+// row per 64-lane workgroup so it can be checked against the oracle alone.
+__global__ void k_mlp_pack_wave(const float* __restrict__ w1t, const float* __restrict__ b1,
+                                const float* __restrict__ w2t, const float* __restrict__ b2,
+                                const float* __restrict__ w3t, const float* __restrict__ b3,
+                                const float* __restrict__ w4t, const float* __restrict__ b4, float* __restrict__ Q) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= MLPW_TOTAL) return;
+  float v;
+  if (i < MLPW_L2) v = mlpw_pack_elem(w1t, MLPW_IN, MLPW_H1, i - MLPW_L1);
+  else if (i < MLPW_L3) v = mlpw_pack_elem(w2t, MLPW_H1, MLPW_H2, i - MLPW_L2);
+  else if (i < MLPW_L4) v = mlpw_pack_elem(w3t, MLPW_H2, MLPW_H3, i - MLPW_L3);
+  else if (i < MLPW_B1) v = mlpw_pack_elem(w4t, MLPW_H3, MLPW_OUT, i - MLPW_L4);
+  else if (i < MLPW_B2) v = b1[i - MLPW_B1];
+  else if (i < MLPW_B3) v = b2[i - MLPW_B2];
+  else if (i < MLPW_B4) v = b3[i - MLPW_B3];
+  else if (i < MLPW_FLAG) v = i - MLPW_B4 < MLPW_OUT ? b4[i - MLPW_B4] : 0.0f;
+  else return;                                         // the flag word (k_mlp_wave_flag)
+  Q[i] = v;
+  // a non-finite weight: every input row must be read (0 * inf is NaN, not a no-op)
+  if (i < MLPW_B1 && !__builtin_isfinite(v)) atomicAnd(reinterpret_cast<uint32_t*>(Q + MLPW_FLAG), 0u);
+}
+__global__ void k_mlp_wave_flag(float* __restrict__ Q) { *reinterpret_cast<uint32_t*>(Q + MLPW_FLAG) = 1u; }
+
+__global__ __launch_bounds__(64) void k_mlp_wave(const float* __restrict__ feat, int M, const float* __restrict__ Q,
+                                                 float* __restrict__ probs, float* __restrict__ logits) {
+  __shared__ __attribute__((aligned(16))) float R[MLPW_R_FLOATS];
+  const long m = blockIdx.x;
+  if (m >= M) return;
+  for (int i = threadIdx.x; i < MLPW_IN + 2; i += 64) R[MLPW_R_X + i] = i < MLPW_IN ? feat[m * MLPW_IN + i] : 0.0f;
+  mlpw_forward(Q, (mlpw_lds_t*)R);
+  if (threadIdx.x < MLPW_OUT) {
+    probs[m * MLPW_OUT + threadIdx.x] = R[MLPW_R_PROBS + threadIdx.x];
+    if (logits) logits[m * MLPW_OUT + threadIdx.x] = R[MLPW_R_LOGITS + threadIdx.x];
+  }
+}
+
 size_t mlp_lds() { return (size_t)MLP_ROWS * (MLP_XS + MLP_H1S) * sizeof(float); }
 bool g_mlp_attr = false;
 
@@ -434,6 +474,25 @@ int cit_mlp_forward_packed(const float* feat, int M, const void* packed, float* 
   hipLaunchKernelGGL((k_mlp_layer<MLP_H1, MLP_H2>), dim3(tiles, MLP_H2 / (16 * MLP_LAYER_WAVES)),
                      dim3(64 * MLP_LAYER_WAVES), 0, stream, h1, M, P + MLP_P2, P + MLP_PB2, h2);
   hipLaunchKernelGGL(k_mlp_head, dim3(tiles), dim3(64 * MLP_HEAD_WAVES), 0, stream, h2, M, P, probs, logits);
+  CHECK_LAUNCH();
+}
+
+size_t cit_mlp_wave_bytes(void) { return (size_t)MLPW_TOTAL * sizeof(float); }
+
+int cit_mlp_pack_wave(const float* w1t, const float* b1, const float* w2t, const float* b2, const float* w3t,
+                      const float* b3, const float* w4t, const float* b4, void* packed, hipStream_t stream) {
+  if (!w1t || !b1 || !w2t || !b2 || !w3t || !b3 || !w4t || !b4 || !packed) return -1;
+  hipLaunchKernelGGL(k_mlp_wave_flag, dim3(1), dim3(1), 0, stream, (float*)packed);
+  hipLaunchKernelGGL(k_mlp_pack_wave, dim3((unsigned)((MLPW_TOTAL + 255) / 256)), dim3(256), 0, stream, w1t, b1, w2t,
+                     b2, w3t, b3, w4t, b4, (float*)packed);
+  CHECK_LAUNCH();
+}
+
+int cit_mlp_forward_wave(const float* feat, int M, const void* packed, float* probs, float* logits,
+                         hipStream_t stream) {
+  if (M < 0 || (M && (!feat || !packed || !probs))) return -1;
+  if (!M) return 0;
+  hipLaunchKernelGGL(k_mlp_wave, dim3(M), dim3(64), 0, stream, feat, M, (const float*)packed, probs, logits);
   CHECK_LAUNCH();
 }
 

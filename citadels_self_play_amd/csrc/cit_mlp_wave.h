@@ -1,0 +1,253 @@
+// Value-MLP forward of ONE row by ONE wavefront: the search's in-kernel leaf
+// evaluation (cfr_pred without suspending the tree, cit_cfr_pred_fused) and
+// its test entry (cit_mlp_forward_wave).
+//
+//   wp = square_and_normalize(fc4(relu(fc3(relu(fc2'(relu(fc1'(x))))))))
+//        (algorithms/models.py:17-24, algorithms/train_utils.py:143-145,
+//         algorithms/deep_mccfr.py:364-374)
+//
+// Lane l owns output columns l, l + 64, ... of every layer and runs each
+// column's k-ordered fmaf chain from 0, then + bias, then ReLU: the arithmetic
+// of oracle/mlp_fma.c and of the MFMA kernels (cit_mlp.hip), so the outputs
+// are bitwise theirs.  One row cannot fill a matrix core, and what bounds a
+// single-row forward is the weight stream, so the chains run on the VALU
+// (v_pk_fma_f32: two columns per instruction) with the weight rows loaded
+// PF rows ahead, and only the rows whose input is non-zero are read:
+//
+// Zero inputs are skipped.  encode_game rows are mostly zero (one-hots and
+// counts: ~60-90 of 418 non-zero) and a ReLU output is exactly +0 for about
+// half the units, and fmaf(0, w, acc) == acc bit for bit whenever w is finite
+// and acc is not -0; a chain's accumulator starts at +0, stays +0 until its
+// first non-zero product and is never -0 afterwards except by underflow of a
+// product smaller than half the least denormal -- and then only its sign of
+// zero could differ, which the bias add (+0 + b == -0 + b for b != 0) and the
+// ReLU / squaring that follow erase.  So the skipped chains equal the full
+// ones; with a non-finite weight (0 * inf = NaN) the pack clears the flag
+// word and every row is read.
+//
+// Weights in the "row layout" (cit_mlp_pack_wave): layer (K, N) as K rows; for
+// N a multiple of 64 row k holds lane l's S = N / 64 columns contiguously
+// ({W[k][64 s + l]}_s at float k * N + l * S: one 16- or 32-byte load per lane,
+// a wave's load is the whole 2 KB / 1 KB / 512 B row); fc4 (N = 6): row k =
+// {W[k][0..5], 0, 0} (8 floats, lanes below 6 read one float each).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define MLPW_HD __host__ __device__
+#else
+#define MLPW_HD
+#endif
+
+#define MLPW_IN 418
+#define MLPW_H1 512
+#define MLPW_H2 256
+#define MLPW_H3 128
+#define MLPW_OUT 6
+
+MLPW_HD constexpr int mlpw_rs(int N) { return N >= 64 ? N : 8; }              // row stride (floats)
+MLPW_HD constexpr long mlpw_floats(int K, int N) { return (long)K * mlpw_rs(N); }
+#define MLPW_L1 0L
+#define MLPW_L2 (MLPW_L1 + mlpw_floats(MLPW_IN, MLPW_H1))
+#define MLPW_L3 (MLPW_L2 + mlpw_floats(MLPW_H1, MLPW_H2))
+#define MLPW_L4 (MLPW_L3 + mlpw_floats(MLPW_H2, MLPW_H3))
+#define MLPW_B1 (MLPW_L4 + mlpw_floats(MLPW_H3, MLPW_OUT))
+#define MLPW_B2 (MLPW_B1 + MLPW_H1)
+#define MLPW_B3 (MLPW_B2 + MLPW_H2)
+#define MLPW_B4 (MLPW_B3 + MLPW_H3)
+#define MLPW_FLAG (MLPW_B4 + 8)              // uint32: 1 = every weight finite (zero inputs may be skipped)
+#define MLPW_TOTAL (MLPW_FLAG + 4)
+
+// The forward's LDS scratch (floats): h1 [0, 512) | x [512, 932) (418 + two
+// zero pads) | layer 1's list of non-zero inputs (int16) from 936 -- layer 1
+// reads x and writes h1 --; then h2 over x with layer 2's list at [768, 1024),
+// h3 over h1, layers 3 / 4's lists at 768, and the logits / probabilities at
+// [1024, 1040).
+#define MLPW_R_H1 0
+#define MLPW_R_X 512
+#define MLPW_R_L1 936
+#define MLPW_R_H2 512
+#define MLPW_R_LN 768
+#define MLPW_R_H3 0
+#define MLPW_R_LOGITS 1024
+#define MLPW_R_PROBS 1032
+#define MLPW_R_FLOATS 1146
+
+// Element e of the row layout of W [K][N] (row-major, k major).
+MLPW_HD inline float mlpw_pack_elem(const float* W, int K, int N, long e) {
+  const int rs = mlpw_rs(N);
+  const int k = (int)(e / rs), i = (int)(e % rs);
+  int c = i;
+  if (N >= 64) {
+    const int S = N / 64, l = i / S, s = i % S;
+    c = 64 * s + l;
+  }
+  return (k < K && c < N) ? W[(long)k * N + c] : 0.0f;
+}
+
+#if defined(__HIPCC__)
+typedef __attribute__((address_space(3))) float mlpw_lds_t;
+typedef __attribute__((address_space(3))) int16_t mlpw_lds_i16;
+typedef float mlpw_f4 __attribute__((ext_vector_type(4)));
+typedef float mlpw_f2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) float mlpw_gf_t;
+
+// a wave-uniform global pointer (scalar base, global_* instructions)
+__device__ __forceinline__ mlpw_gf_t* mlpw_glb(const float* p) {
+  uint64_t a = (uint64_t)(uintptr_t)p;
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  return (mlpw_gf_t*)(((uint64_t)hi << 32) | lo);
+}
+
+// The ascending list of input indices k < K whose x[k] is non-zero (every k
+// when !skip) into `list`; returns its length (wave-uniform).
+template <int K>
+__device__ __forceinline__ int mlpw_list(const mlpw_lds_t* x, mlpw_lds_i16* list, bool skip) {
+  const int lane = __lane_id();
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < K; i += 64) {
+    const int k = i + lane;
+    const bool nz = k < K && (!skip || x[k < K ? k : 0] != 0.0f);
+    const uint64_t m = __ballot(nz);
+    if (nz) list[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = (int16_t)k;
+    n += __popcll(m);
+  }
+  return __builtin_amdgcn_readfirstlane(n);
+}
+
+// S floats of weight row k for this lane (S = 8, 4, 2 or 1).
+template <int S>
+struct mlpw_row {
+  float v[S];
+};
+template <int N>
+__device__ __forceinline__ mlpw_row<(N >= 64 ? N / 64 : 1)> mlpw_ld(const __attribute__((address_space(1))) char* W,
+                                                                     int k, uint32_t voff) {
+  constexpr int S = N >= 64 ? N / 64 : 1;
+  const __attribute__((address_space(1))) char* rb = W + (long)k * (mlpw_rs(N) * 4);     // uniform
+  mlpw_row<S> r;
+  if constexpr (S >= 4) {
+#pragma unroll
+    for (int j = 0; j < S / 4; j++) {
+      const mlpw_f4 q = *(const __attribute__((address_space(1))) mlpw_f4*)(rb + voff + 16 * j);
+      r.v[4 * j] = q.x;
+      r.v[4 * j + 1] = q.y;
+      r.v[4 * j + 2] = q.z;
+      r.v[4 * j + 3] = q.w;
+    }
+  } else if constexpr (S == 2) {
+    const mlpw_f2 q = *(const __attribute__((address_space(1))) mlpw_f2*)(rb + voff);
+    r.v[0] = q.x;
+    r.v[1] = q.y;
+  } else {
+    r.v[0] = *(const __attribute__((address_space(1))) float*)(rb + voff);
+  }
+  return r;
+}
+
+// One layer over the listed inputs: y[c] = act(fmaf chain over the listed k,
+// ascending, of x[k] * W[k][c], from 0, + b[c]) for this lane's columns; the
+// rows (and their x[k]) run PF list entries ahead in a register ring.
+template <int K, int N, int PF, bool RELU>
+__device__ __forceinline__ void mlpw_layer(const float* Wl, const float* bias, const mlpw_lds_t* x,
+                                           const mlpw_lds_i16* list, int nnz, mlpw_lds_t* y) {
+  constexpr int S = N >= 64 ? N / 64 : 1;
+  const int lane = __lane_id();
+  const __attribute__((address_space(1))) char* wb = (const __attribute__((address_space(1))) char*)mlpw_glb(Wl);
+  const uint32_t voff = (uint32_t)(N >= 64 ? lane * S : (lane < N ? lane : N - 1)) * 4u;
+  auto kat = [&](int t) -> int {           // list entry t (clamped; row 0 when the list is empty)
+    return nnz ? __builtin_amdgcn_readfirstlane((int)list[t < nnz ? t : nnz - 1]) : 0;
+  };
+  float acc[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) acc[s] = 0.0f;
+  mlpw_row<S> w[PF];
+  float xr[PF];
+#pragma unroll
+  for (int i = 0; i < PF; i++) {
+    const int k = kat(i);
+    w[i] = mlpw_ld<N>(wb, k, voff);
+    xr[i] = x[k];
+    __builtin_amdgcn_sched_barrier(0);     // issue the ring in list order (the oldest rows are consumed first)
+  }
+#pragma nounroll
+  for (int t0 = 0; t0 < nnz; t0 += PF) {
+#pragma unroll
+    for (int i = 0; i < PF; i++) {
+      if (t0 + i < nnz) {
+        const float xv = xr[i];
+        if constexpr (S == 1) {
+          acc[0] = __builtin_fmaf(xv, w[i].v[0], acc[0]);
+        } else {
+          const mlpw_f2 xx = mlpw_f2{xv, xv};
+#pragma unroll
+          for (int s = 0; s < S; s += 2) {
+            const mlpw_f2 r = __builtin_elementwise_fma(xx, mlpw_f2{w[i].v[s], w[i].v[s + 1]},
+                                                        mlpw_f2{acc[s], acc[s + 1]});
+            acc[s] = r.x;
+            acc[s + 1] = r.y;
+          }
+        }
+        const int k = kat(t0 + i + PF);   // refill the slot PF entries ahead
+        w[i] = mlpw_ld<N>(wb, k, voff);
+        xr[i] = x[k];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  mlpw_gf_t* bp = mlpw_glb(bias);
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const int c = N >= 64 ? 64 * s + lane : lane;
+    if (c < N) {
+      const float v = acc[s] + bp[c];
+      y[c] = RELU ? (v > 0.0f ? v : 0.0f) : v;
+    }
+  }
+}
+
+// The forward over the row at R + MLPW_R_X (MLPW_IN floats) with the
+// row-layout weights Q: logits to R + MLPW_R_LOGITS, probabilities
+// (square_and_normalize, the sum in index order) to R + MLPW_R_PROBS.  The
+// caller's workgroup is this one wavefront; the barriers order the lanes'
+// LDS writes before other lanes read them.
+__device__ __forceinline__ void mlpw_forward(const float* Q, mlpw_lds_t* R) {
+  const bool skip = *(const __attribute__((address_space(1))) uint32_t*)(mlpw_glb(Q) + MLPW_FLAG) != 0u;
+  mlpw_lds_i16* l1 = (mlpw_lds_i16*)(R + MLPW_R_L1);
+  mlpw_lds_i16* ln = (mlpw_lds_i16*)(R + MLPW_R_LN);
+  __syncthreads();
+  int n = mlpw_list<MLPW_IN>(R + MLPW_R_X, l1, skip);
+  __syncthreads();
+  mlpw_layer<MLPW_IN, MLPW_H1, 8, true>(Q + MLPW_L1, Q + MLPW_B1, R + MLPW_R_X, l1, n, R + MLPW_R_H1);
+  __syncthreads();
+  n = mlpw_list<MLPW_H1>(R + MLPW_R_H1, ln, skip);
+  __syncthreads();
+  mlpw_layer<MLPW_H1, MLPW_H2, 12, true>(Q + MLPW_L2, Q + MLPW_B2, R + MLPW_R_H1, ln, n, R + MLPW_R_H2);
+  __syncthreads();
+  n = mlpw_list<MLPW_H2>(R + MLPW_R_H2, ln, skip);
+  __syncthreads();
+  mlpw_layer<MLPW_H2, MLPW_H3, 16, true>(Q + MLPW_L3, Q + MLPW_B3, R + MLPW_R_H2, ln, n, R + MLPW_R_H3);
+  __syncthreads();
+  n = mlpw_list<MLPW_H3>(R + MLPW_R_H3, ln, skip);
+  __syncthreads();
+  mlpw_layer<MLPW_H3, MLPW_OUT, 16, false>(Q + MLPW_L4, Q + MLPW_B4, R + MLPW_R_H3, ln, n, R + MLPW_R_LOGITS);
+  __syncthreads();
+  float sq[MLPW_OUT], s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < MLPW_OUT; j++) {
+    const float v = R[MLPW_R_LOGITS + j];
+    sq[j] = v * v;
+    s += sq[j];
+  }
+  if (__lane_id() < MLPW_OUT) {
+    const int j = __lane_id();
+    float q = sq[0];
+#pragma unroll
+    for (int i = 1; i < MLPW_OUT; i++) q = j == i ? sq[i] : q;
+    R[MLPW_R_PROBS + j] = q / s;
+  }
+  __syncthreads();
+}
+#endif

@@ -86,6 +86,11 @@ PRED_GROUPS = int(os.environ.get("CIT_PRED_GROUPS", "3"))
 # never idles for the host's round turnaround; launches past the end find
 # every tree done and return at once
 PRED_AHEAD = int(os.environ.get("CIT_PRED_AHEAD", "4"))
+# cfr_pred as one launch whose trees evaluate their leaves in their own kernel
+# (cit_cfr_pred_fused, the single-row MLP of cit_mlp_wave.h) instead of rounds
+# of search launches and batched MFMA leaf launches; the trees are bitwise
+# the same either way (tests/test_gpu_mlp.py, tests/test_gpu_configs.py)
+PRED_FUSED = os.environ.get("CIT_PRED_FUSED", "1") != "0"
 PRED_SLICE_TICKS = int(os.environ.get("CIT_PRED_SLICE_TICKS", "0"))   # 1 / 2 / 3 / 4: 87.0k / 96.9k / 100.3k / 61.4k decisions/s (config 4, profiles/r03/pred_groups)
 _side_streams = {}
 
@@ -493,12 +498,15 @@ class GameBatch:
         return (int(h[0]), int(h[2])), (int(h[1]), int(h[3]))
 
     def cfr_pred(self, iters, net, max_depth=10, node_cap=1024, edge_cap=None, max_rounds=100000, max_retries=3,
-                 flags=0, orig=None, groups="auto", slice_ticks="auto"):
+                 flags=0, orig=None, groups="auto", slice_ticks="auto", fused="auto"):
         """run_mccfr(game, model, max_iterations=iters) with a model and training=False
         (cfr_pred(iters, max_depth) + live action choice) on every lane.  `net` is a
-        models.ValueNet; leaf rows of all suspended trees are evaluated in one MFMA
-        launch per round.  Trees that outgrow their pool are searched again with
-        a 4x pool (as cfr_decide).  Returns (chosen, stats [B,5], rounds).
+        models.ValueNet.  fused (auto: PRED_FUSED): one launch, each tree
+        evaluating its leaves in its own kernel (rounds = 0); otherwise leaf rows
+        of all suspended trees are evaluated in one MFMA launch per round.
+        Both search bitwise the same trees.  Trees that outgrow their pool are
+        searched again with a 4x pool (as cfr_decide).  Returns (chosen, stats
+        [B,5], rounds).
 
         groups > 1 (auto: PRED_GROUPS = 3 from 2,048 trees): the trees are split into that many
         sub-batches whose rounds run on their own HIP streams, interleaved, so
@@ -513,8 +521,12 @@ class GameBatch:
         if not hasattr(self, "np_mt"):
             self.seed_numpy()
         snap = self._snapshot() if max_retries > 0 else None
+        F = PRED_FUSED if fused == "auto" else bool(fused)
         G = (PRED_GROUPS if self.B >= PRED_GROUP_MIN else 1) if groups == "auto" else max(1, min(int(groups), self.B))
-        if G > 1:
+        if F:
+            self._groups = None
+            chosen, stats, rounds = self._cfr_pred_fused(iters, net, max_depth, node_cap, edge_cap, flags, orig)
+        elif G > 1:
             chosen, stats, rounds = self._cfr_pred_groups(G, iters, net, max_depth, node_cap, edge_cap, max_rounds,
                                                           flags, orig)
         else:
@@ -524,7 +536,7 @@ class GameBatch:
 
         def run(sub, nc, ec, mr, o):
             c, st, r = sub.cfr_pred(iters, net, max_depth, nc, ec, max_rounds, mr, flags, o,
-                                    slice_ticks=self._slice_ticks)
+                                    slice_ticks=self._slice_ticks, fused=F)
             box[0] += r
             return c, st
         chosen, stats = self._retry_overflow(snap, stats, chosen, run, max_retries, orig)
@@ -542,6 +554,19 @@ class GameBatch:
                       "chosen": torch.zeros((self.B, 16), dtype=torch.uint8, device=d),
                       "waiting": torch.zeros((max(1, PRED_AHEAD), 2), dtype=torch.int32, device=d),
                       "ticks": getattr(self, "_slice_ticks", 0)}       # (waiting, running) per round of a batch
+
+    def _cfr_pred_fused(self, iters, net, max_depth, node_cap, edge_cap, flags=0, orig=None):
+        """cit_cfr_pred_fused: every tree to its decision in one launch."""
+        self._pred_begin(node_cap, edge_cap, orig)
+        P = self._pred
+        o = P["o"]
+        stats = torch.empty((self.B, 5), dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.cit_cfr_pred_fused(
+            _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
+            _ptr(self.seer), self.B, int(iters), int(flags), None if o is None else _ptr(o), int(max_depth),
+            _ptr(self.pool), self.node_cap, self.edge_cap, _ptr(self.optbuf), net.wave.data_ptr(), _ptr(P["state"]),
+            _ptr(P["chosen"]), _ptr(stats), _stream()), "cit_cfr_pred_fused")
+        return P["chosen"], stats.cpu(), 0
 
     def _pred_step(self, iters, max_depth, flags, slot=0):
         """One cit_cfr_pred_step launch (every tree runs to its next leaf evaluation

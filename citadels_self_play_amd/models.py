@@ -67,18 +67,29 @@ class ValueNet:
         self.packed = torch.empty(int(self.lib.cit_mlp_packed_bytes()), dtype=torch.uint8, device=self.device)
         _lib.check(self.lib.cit_mlp_pack(*[t.data_ptr() for t in self.w], self.packed.data_ptr(),
                                          torch.cuda.current_stream(self.device).cuda_stream), "cit_mlp_pack")
+        # the single-row (one wavefront) layout the search kernel evaluates leaves with (cit_cfr_pred_fused)
+        self.wave = torch.empty(int(self.lib.cit_mlp_wave_bytes()), dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.cit_mlp_pack_wave(*[t.data_ptr() for t in self.w], self.wave.data_ptr(),
+                                              torch.cuda.current_stream(self.device).cuda_stream),
+                   "cit_mlp_pack_wave")
 
-    def forward(self, feat, logits=False, fused=False):
+    def forward(self, feat, logits=False, fused=False, wave=False):
         """probs [M][6] (and logits).  Default: the layer-split launches over
         the packed weights (cit_mlp_forward_packed, H1 / H2 in a workspace
         from torch's caching allocator); fused=True: the one-launch k_mlp
-        (cit_mlp_forward).  Both give bitwise the same outputs."""
+        (cit_mlp_forward); wave=True: one row per wavefront on the VALU
+        (cit_mlp_forward_wave, the search kernel's in-place leaf evaluation).
+        All give bitwise the same outputs."""
         feat = feat.contiguous()
         M = feat.shape[0]
         probs = torch.empty((M, 6), dtype=torch.float32, device=self.device)
         lg = torch.empty((M, 6), dtype=torch.float32, device=self.device) if logits else None
         s = torch.cuda.current_stream().cuda_stream
-        if fused:
+        if wave:
+            _lib.check(self.lib.cit_mlp_forward_wave(feat.data_ptr(), M, self.wave.data_ptr(), probs.data_ptr(),
+                                                     lg.data_ptr() if lg is not None else None, s),
+                       "cit_mlp_forward_wave")
+        elif fused:
             ptrs = [t.data_ptr() for t in self.w]
             _lib.check(self.lib.cit_mlp_forward(feat.data_ptr(), M, *ptrs, probs.data_ptr(),
                                                 lg.data_ptr() if lg is not None else None, s), "cit_mlp_forward")

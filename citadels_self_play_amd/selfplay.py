@@ -82,17 +82,18 @@ def broadcast_model(model, src=0):
     return model
 
 
-def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None):
+def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None, fused="auto"):
     """Configs 3/4 (tools/gen_golden_cfr.py harness): per seed s, random.seed(s),
     np.random.seed(s), create_game(), randint(lo, hi) random steps, then
-    run_mccfr(game, net, iters).  Returns (batch, chosen, stats[, rounds])."""
+    run_mccfr(game, net, iters) (fused: GameBatch.cfr_pred's leaf-evaluation
+    mode).  Returns (batch, chosen, stats[, rounds])."""
     b = GameBatch(seeds, preset=True, device=device)
     b.advance_random(lo, hi)
     b.seed_numpy()
     if net is None:
         chosen, stats = b.cfr_decide(iters, node_cap=node_cap or 1024)
         return b, chosen, stats, 0
-    chosen, stats, rounds = b.cfr_pred(iters, net, max_depth=10, node_cap=node_cap or 2048)
+    chosen, stats, rounds = b.cfr_pred(iters, net, max_depth=10, node_cap=node_cap or 2048, fused=fused)
     return b, chosen, stats, rounds
 
 
@@ -270,221 +271,388 @@ def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_c
     Results (stats, targets in seed order, final games and streams) are those
     of simulate_games bit for bit; trees that overflow are searched again
     through GameBatch.cfr_decide (its retry).  Returns (batch of all seeds,
-    stats, targets)."""
-    from .engine import ERR_OVERFLOW, ERR_POOL, ERR_POOL_ARENA, ERR_POOL_CAP, pool_bytes
-    from . import layout as L
-    if node_cap is None:
-        node_cap, ec = pool_caps(iters)
-        edge_cap = edge_cap or ec
-    edge_cap = edge_cap or 5 * node_cap
-    dev = torch.device(device or "cuda")
-    t_setup = time.perf_counter()
-    src = GameBatch(np.asarray(seeds, np.int64), preset=True, device=dev)
-    src.random_position(max_move)
-    src.seed_numpy()
-    term = src.terminal()
-    Q = src.B
-    snap = src._snapshot()
-    if max_pool_bytes is None:
-        torch.cuda.empty_cache()
-        max_pool_bytes = int(0.8 * torch.cuda.mem_get_info(dev)[0])
-    frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
-    S = min(Q, slots or Q)
-    while S > 1 and pool_bytes(S, node_cap, edge_cap, frac(S)) > max_pool_bytes:
-        S = max(1, min(S - 1, int(max_pool_bytes // (pool_bytes(S, node_cap, edge_cap, frac(S)) / S))))
-    if overcommit is None:
-        overcommit = QUEUE_OVERCOMMIT if (arena_frac == "auto" and frac(S) is not None) else 1.0
-    arena_f = frac(S)
-    if overcommit > 1 and arena_f is not None and S < Q:
-        # the same bytes as S trees at ARENA_FRAC, shared by more slots
-        fn, fe = arena_f if isinstance(arena_f, tuple) else (arena_f, arena_f)
-        nbt, ebt = L.cfr_nblocks(node_cap), L.cfr_eblocks(edge_cap)
-        nb0, eb0 = fn * S * nbt, fe * S * ebt
-        S2 = min(Q, int(S * overcommit))
-        from .engine import row_cap_for
-        scale = (max_pool_bytes - S2 * L.cfr_pool_bytes(node_cap, edge_cap)) / float(
-            L.cfr_arena_bytes(int(nb0), int(eb0), row_cap_for(node_cap), False))
-        S, arena_f = S2, (min(1.0, nb0 * scale / (S2 * nbt)), min(1.0, eb0 * scale / (S2 * ebt)))
-    else:
-        overcommit = 1.0
-    sb = src.subset(torch.arange(S, device=dev))
-    sb.arena_frac = arena_f
-    sb._pool(node_cap, edge_cap)
-    planner = _SlicePlanner(sb, node_cap, edge_cap) if overcommit > 1 else None
-    if log is not None:
-        torch.cuda.synchronize()
-        log("simulate_queue: %d positions and a %d-slot pool set up in %.1f s"
-            % (Q, S, time.perf_counter() - t_setup))
-    state = torch.zeros((S, 16), dtype=torch.int32, device=dev)
-    chosen = torch.zeros((S, 16), dtype=torch.uint8, device=dev)
-    stats = torch.zeros((S, 5), dtype=torch.int32, device=dev)
-    running = torch.zeros(1, dtype=torch.int32, device=dev)
-    out_stats = torch.zeros((Q, 5), dtype=torch.int32, device=dev)
-    out_chosen = torch.zeros((Q, 16), dtype=torch.uint8, device=dev)
-    slot_q = torch.arange(S, device=dev)         # queue index held by each slot (-1: idle)
-    parts, nxt, n_slices, n_done = [], S, 0, 0
-    ticks = max(1, int(slice_seconds * 1e8))
-    ran = np.zeros(S, bool)
-    from .engine import side_streams
-    main = torch.cuda.current_stream(dev)
-    side, rstream = side_streams(dev, 2)
-    early = []            # overflowed trees searched again at once, beside the queue: (queue ids, batch, chosen, stats)
-    requeue, retries = [], {}
-    pending = None        # (slots, queue ids) finished last slice: targets extracted during this slice
-    n_requeued = 0
-    # CIT_QUEUE_PROF=1: wall time per phase (synchronising after each; diagnosis only)
-    qprof = {"plan": 0.0, "slice+targets": 0.0, "finish": 0.0} if os.environ.get("CIT_QUEUE_PROF") else None
-    # CIT_QUEUE_TRACE=path: one JSON line per slice (time, live / paused / searching trees, trees done,
-    # arena blocks held) -- where the queue's time goes (diagnosis only)
-    qtrace = open(os.environ["CIT_QUEUE_TRACE"], "w") if os.environ.get("CIT_QUEUE_TRACE") else None
-    t_q0 = time.perf_counter()
+    stats, targets).  One round of a TreeQueue (which can also run rounds
+    back to back, the next round's trees taking the slots the current
+    round's tail leaves)."""
+    q = TreeQueue(iters, len(seeds), slots=slots, max_move=max_move, node_cap=node_cap, edge_cap=edge_cap,
+                  device=device, slice_seconds=slice_seconds, max_pool_bytes=max_pool_bytes, arena_frac=arena_frac,
+                  log=log, overcommit=overcommit, max_requeue=max_requeue, multi_round=False)
+    r = q.add(seeds)
+    q.run(r)
+    out = q.result(r)
+    q.close()
+    return out
 
-    def tick(key, t0):
-        if qprof is None:
+
+class _Round:
+    """One round of positions in a TreeQueue: its source batch (positions,
+    then the finished games and streams), per-tree outputs and target parts."""
+
+    def __init__(self, seeds, base, max_move, dev):
+        self.src = GameBatch(np.asarray(seeds, np.int64), preset=True, device=dev)
+        self.src.random_position(max_move)
+        self.src.seed_numpy()
+        self.term = self.src.terminal()
+        self.Q = self.src.B
+        self.base = base
+        self.snap = self.src._snapshot()
+        self.out_stats = torch.zeros((self.Q, 5), dtype=torch.int32, device=dev)
+        self.out_chosen = torch.zeros((self.Q, 16), dtype=torch.uint8, device=dev)
+        self.parts, self.early = [], []
+        self.n_done = 0          # trees finished (targets walked or pending)
+        self.counted = self.n_walked = self.n_targets = 0   # TreeQueue.targets_so_far's running totals
+        self.t_done = None       # perf_counter when run() saw the round complete
+
+
+class TreeQueue:
+    """simulate_game trees (create_a_random_game(max_move) -> cfr_train(iters)
+    -> get_all_targets) through one tree queue over rounds of positions
+    (train_from_scratch.collect's rounds, the reference's get_mccfr_targets
+    loop, train_from_scratch.py:45-64).  `add(seeds)` appends a round; its
+    trees enter the queue's slots in order after the earlier rounds' trees,
+    so while one round's longest trees finish, the next round's trees already
+    search in the slots (and arena blocks) the finished ones freed.
+    `run(r)` searches until round r is complete, `result(r)` returns it as
+    simulate_queue does (bit-identical to searching the round alone: a
+    tree's search depends only on its own position and streams).  A round
+    that turns out not to be needed is simply never run to its end (close()).
+
+    `per_round` (the trees in one round) sizes the slots: as simulate_queue
+    sizes them for a batch of that many positions."""
+
+    def __init__(self, iters, per_round, slots=None, max_move=100, node_cap=None, edge_cap=None, device=None,
+                 slice_seconds=0.5, max_pool_bytes=None, arena_frac="auto", log=None, overcommit=None,
+                 max_requeue=0, multi_round=True):
+        from .engine import pool_bytes, side_streams, row_cap_for
+        from . import layout as L
+        if node_cap is None:
+            node_cap, ec = pool_caps(iters)
+            edge_cap = edge_cap or ec
+        edge_cap = edge_cap or 5 * node_cap
+        self.iters, self.node_cap, self.edge_cap, self.max_move, self.log = iters, node_cap, edge_cap, max_move, log
+        self.max_requeue, self.multi_round = max_requeue, multi_round
+        dev = self.dev = torch.device(device or "cuda")
+        self.t_setup = time.perf_counter()
+        if max_pool_bytes is None:
+            torch.cuda.empty_cache()
+            max_pool_bytes = int(0.8 * torch.cuda.mem_get_info(dev)[0])
+        frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
+        Q = max(1, int(per_round))
+        S = min(Q, slots or Q)
+        while S > 1 and pool_bytes(S, node_cap, edge_cap, frac(S)) > max_pool_bytes:
+            S = max(1, min(S - 1, int(max_pool_bytes // (pool_bytes(S, node_cap, edge_cap, frac(S)) / S))))
+        if overcommit is None:
+            overcommit = QUEUE_OVERCOMMIT if (arena_frac == "auto" and frac(S) is not None) else 1.0
+        arena_f = frac(S)
+        if overcommit > 1 and arena_f is not None and S < Q:
+            # the same bytes as S trees at ARENA_FRAC, shared by more slots
+            fn, fe = arena_f if isinstance(arena_f, tuple) else (arena_f, arena_f)
+            nbt, ebt = L.cfr_nblocks(node_cap), L.cfr_eblocks(edge_cap)
+            nb0, eb0 = fn * S * nbt, fe * S * ebt
+            S2 = min(Q, int(S * overcommit))
+            scale = (max_pool_bytes - S2 * L.cfr_pool_bytes(node_cap, edge_cap)) / float(
+                L.cfr_arena_bytes(int(nb0), int(eb0), row_cap_for(node_cap), False))
+            S, arena_f = S2, (min(1.0, nb0 * scale / (S2 * nbt)), min(1.0, eb0 * scale / (S2 * ebt)))
+        else:
+            overcommit = 1.0
+        self.S, self.overcommit = S, overcommit
+        self.sb = None
+        self.arena_f = arena_f
+        self.rounds = []
+        self.total = 0                        # positions added over all rounds (global queue ids)
+        self.nxt = 0                          # next global id to admit
+        self.state = torch.zeros((S, 16), dtype=torch.int32, device=dev)
+        self.state[:, 6] = CP_DONE            # an idle slot searches nothing (a slot taking a tree is zeroed)
+        self.chosen = torch.zeros((S, 16), dtype=torch.uint8, device=dev)
+        self.stats = torch.zeros((S, 5), dtype=torch.int32, device=dev)
+        self.running = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.slot_q = torch.full((S,), -1, dtype=torch.long, device=dev)    # global id per slot (-1 idle, -2 walk pending)
+        self.pending = None                   # (slots, global ids) finished last slice: targets walked during this one
+        self.requeue, self.retries = [], {}
+        self.n_slices = self.n_requeued = 0
+        self.ticks = max(1, int(slice_seconds * 1e8))
+        self.ran = np.zeros(S, bool)
+        self.side, self.rstream = side_streams(dev, 2)
+        self.planner = None
+        # CIT_QUEUE_PROF=1: wall time per phase (synchronising after each; diagnosis only)
+        self.qprof = {"plan": 0.0, "slice+targets": 0.0, "finish": 0.0} if os.environ.get("CIT_QUEUE_PROF") else None
+        # CIT_QUEUE_TRACE=path: one JSON line per slice (time, live / paused / searching trees, trees done,
+        # arena blocks held) -- where the queue's time goes (diagnosis only)
+        self.qtrace = open(os.environ["CIT_QUEUE_TRACE"], "w") if os.environ.get("CIT_QUEUE_TRACE") else None
+        self.t_q0 = time.perf_counter()
+
+    # ---------------------------------------------------------------- rounds
+    def add(self, seeds):
+        """Append a round of positions (random.seed(s), np.random.seed(s),
+        create_a_random_game(max_move) per seed); returns its index."""
+        r = _Round(seeds, self.total, self.max_move, self.dev)
+        self.total += r.Q
+        self.rounds.append(r)
+        if self.sb is None:
+            # the slots' batch and pool, shaped from the first round's lanes
+            sb = r.src.subset(torch.arange(min(self.S, r.Q), device=self.dev))
+            if sb.B < self.S:
+                sb = GameBatch.from_tensors(*[t for t in _pad_lanes(sb, self.S)])
+            sb.arena_frac = self.arena_f
+            sb._pool(self.node_cap, self.edge_cap)
+            self.sb = sb
+            # the planner keeps a queue of large trees inside its arena: overcommitted slots, and the
+            # trees of later rounds entering beside a round's tail
+            self.planner = _SlicePlanner(sb, self.node_cap, self.edge_cap) if (
+                self.overcommit > 1 or (self.arena_f is not None and self.multi_round)) else None
+            if self.log is not None:
+                torch.cuda.synchronize()
+                self.log("simulate_queue: %d positions and a %d-slot pool set up in %.1f s"
+                         % (r.Q, self.S, time.perf_counter() - self.t_setup))
+        self._admit()
+        return len(self.rounds) - 1
+
+    def _round_of(self, g):
+        for r in self.rounds:
+            if r.base <= g < r.base + r.Q:
+                return r
+        raise KeyError(g)
+
+    def _split(self, ids, slots=None):
+        """Global ids (device long) -> [(round, local ids, matching slots)]."""
+        out = []
+        for r in self.rounds:
+            m = (ids >= r.base) & (ids < r.base + r.Q)
+            if bool(m.any()):
+                out.append((r, ids[m] - r.base, None if slots is None else slots[m]))
+        return out
+
+    def _admit(self):
+        """Idle slots take the next positions (after the initial fill: slots
+        freed by finished trees take them in _finish)."""
+        idle = (self.slot_q == -1).nonzero().flatten()
+        if idle.numel():
+            self._fill(idle)
+
+    def _fill(self, fs):
+        ids = self.requeue[:int(fs.numel())]
+        del self.requeue[:len(ids)]
+        take = min(int(fs.numel()) - len(ids), self.total - self.nxt)
+        ids += list(range(self.nxt, self.nxt + take))
+        self.nxt += take
+        k = len(ids)
+        if k:
+            new_q = torch.tensor(ids, dtype=torch.long, device=self.dev)
+            for r, loc, sl in self._split(new_q, fs[:k]):
+                self.sb.scatter(r.src.subset(loc), sl)
+            self.state[fs[:k]] = 0
+            if self.planner is not None:
+                self.planner.reset(fs[:k].cpu().numpy())
+            self.slot_q[fs[:k]] = new_q
+        self.slot_q[fs[k:]] = -1
+        self.state[fs[k:], 6] = CP_DONE
+
+    def targets_so_far(self, r):
+        """(trees of round r whose targets were walked, targets they yielded):
+        host counts for deciding whether another round will be needed."""
+        R = self.rounds[r]
+        while R.counted < len(R.parts):
+            t, slots, ids = R.parts[R.counted]
+            R.n_targets += int(t["counts"][slots.long(), 0].sum())
+            R.n_walked += int(slots.numel())
+            R.counted += 1
+        return R.n_walked, R.n_targets
+
+    def done(self, r):
+        R = self.rounds[r]
+        return R.n_done == R.Q and not self._pending_in(R)
+
+    def _pending_in(self, R):
+        if self.pending is None:
+            return False
+        q = self.pending[1]
+        return bool(((q >= R.base) & (q < R.base + R.Q)).any())
+
+    # ----------------------------------------------------------------- slices
+    def _tick(self, key, t0):
+        if self.qprof is None:
             return t0
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        qprof[key] += t1 - t0
+        self.qprof[key] += t1 - t0
         return t1
 
-    def next_ids(k):
-        nonlocal nxt
-        ids = requeue[:k]
-        del requeue[:k]
-        take = min(k - len(ids), Q - nxt)
-        ids += list(range(nxt, nxt + take))
-        nxt += take
-        return ids
-    tq = time.perf_counter()
-    while True:
-        running.zero_()
-        paused = None
-        if planner is not None:
-            st_np = state.cpu().numpy()
-            live = (slot_q.cpu().numpy() >= 0) & (st_np[:, 6] != CP_DONE)
-            pmask = planner.plan(st_np, live, ran)
-            ran = live & ~pmask
-            if pmask.any():
-                paused = torch.from_numpy(np.flatnonzero(pmask)).to(dev)
-                saved = state[paused, 6].clone()
-                state[paused, 6] = CP_DONE           # sits this slice out (the kernel returns at once)
-        tq = tick("plan", tq)
-        sb.train_slice(iters, state, ticks, chosen, stats, running)
-        n_slices += 1
-        if pending is not None:
-            # last slice's finished trees: their targets are walked on a second stream while this
-            # slice runs (their slots sit this slice out, their blocks stay held until the walk ends)
-            p_slots, p_qs = pending
-            with torch.cuda.stream(side):           # (everything it reads was complete at the last sync)
-                roots = torch.full((S,), -1, dtype=torch.int32, device=dev)
-                roots[p_slots] = _roots_for_targets(out_stats[p_qs])
-                parts.append((sb._cfr_targets(roots, 0), p_slots, p_qs))
+    def run(self, r=None, on_slice=None):
+        """Slices until round r (default: every round added) is complete;
+        on_slice(queue) after each slice (may add rounds)."""
+        from .engine import ERR_OVERFLOW, ERR_POOL, ERR_POOL_ARENA
+        sb, state, dev, S = self.sb, self.state, self.dev, self.S
+        tq = time.perf_counter()
+        while True:
+            self._stamp()
+            if r is not None and self.done(r):
+                break
+            self.running.zero_()
+            paused = None
+            if self.planner is not None:
+                st_np = state.cpu().numpy()
+                live = (self.slot_q.cpu().numpy() >= 0) & (st_np[:, 6] != CP_DONE)
+                pmask = self.planner.plan(st_np, live, self.ran)
+                self.ran = live & ~pmask
+                if pmask.any():
+                    paused = torch.from_numpy(np.flatnonzero(pmask)).to(dev)
+                    saved = state[paused, 6].clone()
+                    state[paused, 6] = CP_DONE           # sits this slice out (the kernel returns at once)
+            tq = self._tick("plan", tq)
+            sb.train_slice(self.iters, state, self.ticks, self.chosen, self.stats, self.running)
+            self.n_slices += 1
+            if self.pending is not None:
+                # last slice's finished trees: their targets are walked on a second stream while this
+                # slice runs (their slots sit this slice out, their blocks stay held until the walk ends)
+                p_slots, p_qs = self.pending
+                with torch.cuda.stream(self.side):      # (everything it reads was complete at the last sync)
+                    roots = torch.full((S,), -1, dtype=torch.int32, device=dev)
+                    for R, loc, sl in self._split(p_qs, p_slots):
+                        roots[sl] = _roots_for_targets(R.out_stats[loc])
+                    t = sb._cfr_targets(roots, 0)
+                    for R, loc, sl in self._split(p_qs, p_slots):
+                        R.parts.append((t, sl, loc))
+            torch.cuda.synchronize()
+            tq = self._tick("slice+targets", tq)
+            if paused is not None:
+                state[paused, 6] = saved
+                self.running += int(paused.numel())       # paused trees are unfinished
+            free = []
+            if self.pending is not None:
+                p_slots, p_qs = self.pending
+                for R, loc, sl in self._split(p_qs, p_slots):
+                    R.src.scatter(sb.subset(sl), loc)
+                sb.release(p_slots)
+                free.append(p_slots)
+                self.pending = None
+            done = ((state[:, 6] == CP_DONE) & (self.slot_q >= 0)).nonzero().flatten()
+            if done.numel():
+                qs = self.slot_q[done]
+                st_done = self.stats[done]
+                # max_requeue > 0: a tree stopped only by the shared arena running out starts again
+                # from its position later in the queue (the same search, bit for bit; at most
+                # max_requeue times, then the final retry)
+                redo = torch.zeros(done.numel(), dtype=torch.bool, device=dev)
+                (n_used, e_used), (n_cap, e_cap) = sb.arena_used() if self.max_requeue else ((0, 0), (1, 1))
+                if n_used > n_cap or e_used > e_cap:
+                    st_np = st_done.cpu().numpy()
+                    for i, (q, row) in enumerate(zip(qs.cpu().tolist(), st_np)):
+                        if row[4] == ERR_OVERFLOW | ERR_POOL_ARENA and self.retries.get(q, 0) < self.max_requeue:
+                            self.retries[q] = self.retries.get(q, 0) + 1
+                            redo[i] = True
+                            self.requeue.append(q)
+                            self.n_requeued += 1
+                fin = ~redo
+                ov = fin & ((st_done[:, 4] & ERR_POOL) != 0)        # pool overflows: searched again
+                if bool(ov.any()):
+                    for R, loc, sl in self._split(qs[ov]):
+                        R.early.append(_early_retry(R.snap, loc, st_done[ov][(qs[ov] >= R.base) &
+                                                                             (qs[ov] < R.base + R.Q)],
+                                                    self.iters, self.node_cap, self.edge_cap, self.rstream))
+                    if self.log is not None:
+                        self.log("simulate_queue: tree(s) %s overflowed after slice %d (nodes, edges: %s of caps %d, "
+                                 "%d); searched again beside the queue"
+                                 % (qs[ov].tolist(), self.n_slices, st_done[ov][:, 1:3].tolist(), self.node_cap,
+                                    self.edge_cap))
+                if bool(fin.any()):
+                    qf, sf = qs[fin], st_done[fin]
+                    cf = self.chosen[done[fin]]
+                    for R in self.rounds:
+                        m = (qf >= R.base) & (qf < R.base + R.Q)
+                        if bool(m.any()):
+                            R.out_stats[qf[m] - R.base] = sf[m]
+                            R.out_chosen[qf[m] - R.base] = cf[m]
+                            R.n_done += int(m.sum())
+                    self.pending = (done[fin], qf)
+                    self.slot_q[done[fin]] = -2                 # held: targets pending
+                if bool(redo.any()):
+                    sb.release(done[redo])
+                    free.append(done[redo])
+                    self.slot_q[done[redo]] = -1
+                if self.log is not None:
+                    self.log("simulate_queue: %s trees done after %d slices"
+                             % (" + ".join("%d of %d" % (R.n_done, R.Q) for R in self.rounds), self.n_slices))
+            if free:
+                self._fill(torch.cat(free))
+            if on_slice is not None:
+                on_slice(self)
+            tq = self._tick("finish", tq)
+            if self.qtrace is not None:
+                held = self.planner.held().sum(0).tolist() if self.planner is not None else None
+                self.qtrace.write(json.dumps({
+                    "slice": self.n_slices, "t": round(time.perf_counter() - self.t_q0, 4),
+                    "slots_busy": int((self.slot_q >= 0).sum()), "searching": int(self.ran.sum()),
+                    "paused": 0 if paused is None else int(paused.numel()),
+                    "done": [R.n_done for R in self.rounds], "held_blocks": held,
+                    "arena_blocks": None if self.planner is None else self.planner.cap.tolist()}) + "\n")
+            if (int(self.running.item()) == 0 and self.pending is None and bool((self.slot_q < 0).all())
+                    and not self.requeue):
+                break
+        self._stamp()
+
+    def _stamp(self):
+        for R in self.rounds:
+            if R.t_done is None and R.n_done == R.Q and not self._pending_in(R):
+                R.t_done = time.perf_counter()
+
+    def result(self, r):
+        """(batch of round r's positions, stats, targets) once run(r) returned:
+        the trees that overflowed are settled first (the early retries beside
+        the queue, cfr_decide's retries for any still overflowing)."""
+        from .engine import ERR_POOL
+        R = self.rounds[r]
+        dev = self.dev
+        if self.log is not None and self.planner is not None:
+            self.log("simulate_queue: %d slots (overcommit %.2f), %d tree-slices paused, %d trees restarted after "
+                     "the arena ran out" % (self.S, self.overcommit, self.planner.paused_slices, self.n_requeued))
+        if self.log is not None and self.qprof is not None:
+            self.log("simulate_queue phases (s): %s over %d slices"
+                     % ({k: round(v, 2) for k, v in self.qprof.items()}, self.n_slices))
+        t_retry = time.perf_counter()
+        keep_from = len(R.parts)
         torch.cuda.synchronize()
-        tq = tick("slice+targets", tq)
-        if paused is not None:
-            state[paused, 6] = saved
-            running += int(paused.numel())         # paused trees are unfinished
-        free = []
-        if pending is not None:
-            p_slots, p_qs = pending
-            src.scatter(sb.subset(p_slots), p_qs)
-            sb.release(p_slots)
-            free.append(p_slots)
-            pending = None
-        done = ((state[:, 6] == CP_DONE) & (slot_q >= 0)).nonzero().flatten()
-        if done.numel():
-            qs = slot_q[done]
-            st_done = stats[done]
-            # max_requeue > 0: a tree stopped only by the shared arena running out starts again
-            # from its position later in the queue (the same search, bit for bit; at most
-            # max_requeue times, then the final retry)
-            redo = torch.zeros(done.numel(), dtype=torch.bool, device=dev)
-            (n_used, e_used), (n_cap, e_cap) = sb.arena_used() if max_requeue else ((0, 0), (1, 1))
-            if n_used > n_cap or e_used > e_cap:
-                st_np = st_done.cpu().numpy()
-                for i, (q, row) in enumerate(zip(qs.cpu().tolist(), st_np)):
-                    if row[4] == ERR_OVERFLOW | ERR_POOL_ARENA and retries.get(q, 0) < max_requeue:
-                        retries[q] = retries.get(q, 0) + 1
-                        redo[i] = True
-                        requeue.append(q)
-                        n_requeued += 1
-            fin = ~redo
-            ov = fin & ((st_done[:, 4] & ERR_POOL) != 0)        # pool overflows: searched again
-            if bool(ov.any()):
-                early.append(_early_retry(snap, qs[ov], st_done[ov], iters, node_cap, edge_cap, rstream))
-                if log is not None:
-                    log("simulate_queue: tree(s) %s overflowed after slice %d (nodes, edges: %s of caps %d, %d); "
-                        "searched again beside the queue" % (qs[ov].tolist(), n_slices, st_done[ov][:, 1:3].tolist(),
-                                                             node_cap, edge_cap))
-            if bool(fin.any()):
-                out_stats[qs[fin]] = st_done[fin]
-                out_chosen[qs[fin]] = chosen[done[fin]]
-                pending = (done[fin], qs[fin])
-                slot_q[done[fin]] = -2                 # held: targets pending
-                n_done += int(fin.sum())
-            if bool(redo.any()):
-                sb.release(done[redo])
-                free.append(done[redo])
-                slot_q[done[redo]] = -1
-            if log is not None:
-                log("simulate_queue: %d of %d trees done after %d slices" % (n_done, Q, n_slices))
-        if free:
-            fs = torch.cat(free)
-            ids = next_ids(int(fs.numel()))
-            k = len(ids)
-            if k:
-                new_q = torch.tensor(ids, dtype=torch.long, device=dev)
-                sb.scatter(src.subset(new_q), fs[:k])
-                state[fs[:k]] = 0
-                if planner is not None:
-                    planner.reset(fs[:k].cpu().numpy())
-                slot_q[fs[:k]] = new_q
-            slot_q[fs[k:]] = -1
-        tq = tick("finish", tq)
-        if qtrace is not None:
-            held = planner.held().sum(0).tolist() if planner is not None else None
-            qtrace.write(json.dumps({"slice": n_slices, "t": round(time.perf_counter() - t_q0, 4),
-                                     "slots_busy": int((slot_q >= 0).sum()), "searching": int(ran.sum()),
-                                     "paused": 0 if paused is None else int(paused.numel()), "done": n_done,
-                                     "held_blocks": held, "arena_blocks": None if planner is None
-                                     else planner.cap.tolist()}) + "\n")
-        if int(running.item()) == 0 and pending is None and bool((slot_q < 0).all()) and not requeue:
-            break
-    if log is not None and planner is not None:
-        log("simulate_queue: %d slots (overcommit %.2f), %d tree-slices paused, %d trees restarted after the "
-            "arena ran out" % (S, overcommit, planner.paused_slices, n_requeued))
-    if qtrace is not None:
-        qtrace.close()
-    if log is not None and qprof is not None:
-        log("simulate_queue phases (s): %s over %d slices" % ({k: round(v, 2) for k, v in qprof.items()}, n_slices))
-    sb.pool = None
-    t_retry = time.perf_counter()
-    keep_from = len(parts)
-    torch.cuda.synchronize()
-    over = []
-    for oq, sub, c2, st2 in early:
-        # still overflowing (the early search had 4x caps at most): cfr_decide's retries from the snapshot
-        if bool(((st2[:, 4] & ERR_POOL) != 0).any()):
-            g, mt, idx, seer, npm, npi, steps = snap
-            sub = GameBatch.from_tensors(g[oq].contiguous(), mt[:, oq].contiguous(), idx[oq].contiguous(),
-                                         seer[oq].contiguous(), npm[:, oq].contiguous(), npi[oq].contiguous())
-            sub.row_cap = 0
-            c2, st2 = sub.cfr_decide(iters, node_cap, edge_cap)
-        out_stats[oq] = st2
-        out_chosen[oq] = c2
-        parts.append((sub.cfr_targets(_roots_for_targets(st2), 0), torch.arange(sub.B, device=dev), oq))
-        src.scatter(sub, oq)
-        over.append(oq)
-    over = torch.cat(over) if over else torch.zeros(0, dtype=torch.long, device=dev)
-    if log is not None and over.numel():
-        torch.cuda.synchronize()
-        log("simulate_queue: %d trees overflowed and were searched again beside the queue (%.1f s after it)"
-            % (int(over.numel()), time.perf_counter() - t_retry))
-    t = _assemble_targets(parts, Q, exclude=over, keep_from=keep_from)
-    t["terminal"] = term
-    t["overflow"] = _overflowed(out_stats)
-    t["chosen"] = out_chosen
-    return src, out_stats, t
+        over = []
+        for oq, sub, c2, st2 in R.early:
+            # still overflowing (the early search had 4x caps at most): cfr_decide's retries from the snapshot
+            if bool(((st2[:, 4] & ERR_POOL) != 0).any()):
+                g, mt, idx, seer, npm, npi, steps = R.snap
+                sub = GameBatch.from_tensors(g[oq].contiguous(), mt[:, oq].contiguous(), idx[oq].contiguous(),
+                                             seer[oq].contiguous(), npm[:, oq].contiguous(), npi[oq].contiguous())
+                sub.row_cap = 0
+                c2, st2 = sub.cfr_decide(self.iters, self.node_cap, self.edge_cap)
+            R.out_stats[oq] = st2
+            R.out_chosen[oq] = c2
+            R.parts.append((sub.cfr_targets(_roots_for_targets(st2), 0), torch.arange(sub.B, device=dev), oq))
+            R.src.scatter(sub, oq)
+            over.append(oq)
+        R.early = []
+        over = torch.cat(over) if over else torch.zeros(0, dtype=torch.long, device=dev)
+        if self.log is not None and over.numel():
+            torch.cuda.synchronize()
+            self.log("simulate_queue: %d trees overflowed and were searched again beside the queue (%.1f s after it)"
+                     % (int(over.numel()), time.perf_counter() - t_retry))
+        t = _assemble_targets(R.parts, R.Q, exclude=over, keep_from=keep_from)
+        t["terminal"] = R.term
+        t["overflow"] = _overflowed(R.out_stats)
+        t["chosen"] = R.out_chosen
+        return R.src, R.out_stats, t
+
+    def close(self):
+        if self.qtrace is not None:
+            self.qtrace.close()
+            self.qtrace = None
+        if self.sb is not None:
+            torch.cuda.synchronize()
+            self.sb.pool = None
+            self.sb = None
+
+
+def _pad_lanes(b, S):
+    """The state tensors of batch b padded to S lanes (repeating lane 0): the
+    slot batch of a queue whose first round has fewer trees than slots."""
+    idx = torch.cat([torch.arange(b.B, device=b.device), torch.zeros(S - b.B, dtype=torch.long, device=b.device)])
+    return (b.games[idx].contiguous(), b.mt[:, idx].contiguous(), b.mt_idx[idx].contiguous(),
+            b.seer[idx].contiguous(), b.np_mt[:, idx].contiguous(), b.np_idx[idx].contiguous())
 
 
 def _early_retry(snap, oq, st, iters, node_cap, edge_cap, stream):
@@ -516,29 +684,34 @@ def _overflowed(stats):
 
 
 ERROR_CLASSES = ("value_error", "terminal", "capacity", "pool")
+ERR_UNSUPPORTED = 0x40       # CIT_ERR_UNSUPPORTED (csrc/cit_core.h): an engine limit, not a reference exception
 
 
 def error_classes(stats, terminal):
     """Per-lane class of a tree that yields no targets (-1: none) and the count
     of each class, in ERROR_CLASSES order:
       value_error  the search raised one of the reference's own exceptions
-                   (CIT_ERR_* other than the overflow bit: a ValueError from
-                   np.random.choice over an empty or NaN row, ...);
+                   (CIT_ERR_* other than the overflow and unsupported bits: a
+                   ValueError from np.random.choice over an empty or NaN row,
+                   ...);
       terminal     the position was already over (run_mccfr raises on it);
-      capacity     an engine list overflowed (CIT_ERR_OVERFLOW without a pool
-                   bit): only a player holding more than 88 cards, or more
-                   than 32 hand-knowledge entries, can -- the reference has no
-                   such limit;
+      capacity     an engine limit the reference does not have: a list
+                   overflowed (CIT_ERR_OVERFLOW without a pool bit: a player
+                   holding more than 88 cards, or more than 32 hand-knowledge
+                   entries), or a branch the engine stops on
+                   (CIT_ERR_UNSUPPORTED: the magician / cardinal option tables
+                   of a hand over 32 cards);
       pool         a node pool still overflowed after its retries."""
     from .engine import ERR_OVERFLOW, ERR_POOL
     err = stats[:, 4].cpu()
     term = terminal.cpu().to(torch.bool)
     over = (err & ERR_OVERFLOW) != 0
     pool = over & ((err & ERR_POOL) != 0)
+    unsup = (err & ERR_UNSUPPORTED) != 0
     cls = torch.full(err.shape, -1, dtype=torch.int64)
-    cls[(err != 0) & ~over] = 0
+    cls[(err != 0) & ~over & ~unsup] = 0
     cls[term] = 1
-    cls[over & ~pool & ~term] = 2
+    cls[((over & ~pool) | (unsup & ~over)) & ~term] = 2
     cls[pool & ~term] = 3
     return cls, {k: int((cls == i).sum()) for i, k in enumerate(ERROR_CLASSES)}
 

@@ -5,9 +5,11 @@ process per GPU:
 
 Each data round, every rank runs `--games-per-gpu` simulate_game trees
 (create_a_random_game(100) -> cfr_train(iters, training=True) ->
-get_all_targets) through selfplay.simulate_games (a tree queue over ~1,300
-slots sharing a block arena of ~0.8 of HBM, the least advanced trees paused
-for a slice when it runs short); the (encode_game,
+get_all_targets) through one selfplay.TreeQueue per phase (a tree queue over
+as many slots as its block arena -- ~0.8 of HBM -- holds, the least advanced
+trees paused for a slice when it runs short; when a round's finished trees
+project that another round will be needed, that round's trees enter the
+slots the current round's tail frees); the (encode_game,
 node_value) pairs are pooled across ranks with an RCCL all-gather until
 `--min-targets` are collected (get_mccfr_targets, :45-63).  Rank 0 trains the
 value net (train.train_node_value_only) and the weights are broadcast.  The
@@ -64,16 +66,64 @@ def lane_errors(stats, t, seeds):
     return counts, first_ref, first_eng
 
 
+def round_seeds(args, world, phase, rnd):
+    """This rank's seeds of data round `rnd` of `phase` (a disjoint block per round and rank)."""
+    base = args.seed + (phase * 1000 + rnd) * args.games_per_gpu * world
+    return selfplay.shard(args.games_per_gpu * world, base_seed=base)
+
+
+class _Lookahead:
+    """collect's cross-round queue (selfplay.TreeQueue): while round r's
+    longest trees finish, round r + 1's trees already search in the slots the
+    finished ones freed -- once the targets of round r's finished trees
+    project that the pooled targets will still fall short of min_targets
+    (the estimate only decides whether to start the next round early: the
+    rounds actually used are decided by the pooled count, as in the
+    reference, and a round started but not needed is dropped).  Each round's
+    trees and targets are those of simulate_games on its seeds, bit for bit."""
+
+    def __init__(self, args, world, phase, min_targets, log):
+        self.args, self.world, self.phase, self.min_targets = args, world, phase, min_targets
+        self.q = selfplay.TreeQueue(args.iters, args.games_per_gpu, max_move=100, node_cap=args.node_cap, log=log)
+        self.pooled = 0
+        self.speculated = 0
+
+    def round(self, rnd):
+        while len(self.q.rounds) <= rnd:
+            self.q.add(round_seeds(self.args, self.world, self.phase, len(self.q.rounds)))
+
+        def maybe_next(q):
+            if len(q.rounds) > rnd + 1:
+                return
+            walked, n = q.targets_so_far(rnd)
+            Q = q.rounds[rnd].Q
+            if walked < Q // 2:
+                return
+            projected = self.pooled + n / max(1, walked) * Q * self.world
+            if projected < 1.25 * self.min_targets:
+                q.add(round_seeds(self.args, self.world, self.phase, rnd + 1))
+                self.speculated += 1
+        self.q.run(rnd, on_slice=maybe_next)
+        return self.q.result(rnd)
+
+    def close(self):
+        self.q.close()
+
+
 def collect(rank, world, args, phase, min_targets, log):
     feats, values, tuples = [], [], []
     dropped = {k: 0 for k in selfplay.ERROR_CLASSES}
     pooled = 0
     rnd = 0
+    look = _Lookahead(args, world, phase, min_targets, log) if getattr(args, "lookahead", True) else None
     while pooled < min_targets:
-        base = args.seed + (phase * 1000 + rnd) * args.games_per_gpu * world
-        seeds = selfplay.shard(args.games_per_gpu * world, base_seed=base)
+        seeds = round_seeds(args, world, phase, rnd)
         t0 = time.time()
-        b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap, log=log)
+        if look is None:
+            b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap, log=log)
+        else:
+            look.pooled = pooled
+            b, stats, t = look.round(rnd)
         counts, first_ref, first_eng = lane_errors(stats, t, seeds)
         if args.on_error == "raise":
             bad = torch.tensor([0 if first_ref is None else 1, 0 if first_eng is None else 1], device=stats.device)
@@ -100,6 +150,8 @@ def collect(rank, world, args, phase, min_targets, log):
             "%.1fs" % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, rank, counts["value_error"],
                        counts["terminal"], counts["capacity"], counts["pool"], time.time() - t0))
         rnd += 1
+    if look is not None:
+        look.close()
     collect.dropped = dropped
     return torch.cat(feats), torch.cat(values), tuples
 
@@ -107,9 +159,9 @@ def collect(rank, world, args, phase, min_targets, log):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200000)
-    # 160 cfr_train(200000) pools (~1.3 GB each, engine.pool_caps) fill ~210 GB of
-    # simulate_games runs as many 200k-iteration trees at once as the 288 GB HBM3E
-    # holds (~320) and queues the rest (selfplay.simulate_queue)
+    # the tree queue runs as many 200k-iteration trees at once as the 288 GB HBM3E
+    # holds (all 1,920 of the bench's config 5 at ~0.5 KB per node)
+    # and queues the rest (selfplay.TreeQueue)
     ap.add_argument("--games-per-gpu", type=int, default=960)
     ap.add_argument("--node-cap", type=int, default=None)
     ap.add_argument("--pretrain-targets", type=int, default=20000)
@@ -121,6 +173,9 @@ def main(argv=None):
     ap.add_argument("--out", default=".")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--save-tuples", action="store_true")
+    ap.add_argument("--no-lookahead", dest="lookahead", action="store_false",
+                    help="one simulate_games call per data round instead of one tree queue across rounds (the next "
+                         "round's trees taking the slots the current round's tail frees; same targets)")
     ap.add_argument("--on-error", choices=("drop", "raise"), default="drop",
                     help="a tree whose search raises one of the reference's exceptions (ValueError: an empty or NaN "
                          "choice; a terminal position): drop it and count it (default), or stop the run as the "

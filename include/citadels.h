@@ -51,7 +51,7 @@ typedef struct CitOption {
   uint64_t x;
 } CitOption;
 
-int cit_abi_version(void);              /* 7: diff rows as edge-slot runs (CfrNode.row), opponent edge runs that grow; 6: per-player card areas (hand / just-drawn / museum share 88 slots); 5: packed value-MLP path */
+int cit_abi_version(void);              /* 8: cfr_pred as one launch with in-kernel leaf evaluation (cit_cfr_pred_fused, cit_mlp_*_wave); 7: diff rows as edge-slot runs (CfrNode.row), opponent edge runs that grow; 6: per-player card areas (hand / just-drawn / museum share 88 slots); 5: packed value-MLP path */
 int cit_game_bytes(void);              /* row width of `games` */
 int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
 int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
@@ -172,6 +172,21 @@ int cit_mlp_pack(const float* w1t, const float* b1, const float* w2t, const floa
 size_t cit_mlp_work_bytes(int M);
 int cit_mlp_forward_packed(const float* feat, int M, const void* packed, float* probs, float* logits, void* work,
                            size_t work_bytes, hipStream_t stream);
+/* The same forward, bitwise equal, for ONE row per 64-lane wavefront: lane l
+ * runs the fmaf chains of output columns l, l + 64, ... on the VALU over the
+ * "row layout" of the weights (cit_mlp_pack_wave into cit_mlp_wave_bytes()
+ * bytes: per layer K rows, each lane's columns of a row contiguous, then the
+ * biases and a flag word), reading only the rows whose input is non-zero (a
+ * zero input leaves every finite chain bit-identical; a non-finite weight
+ * clears the flag and every row is read).  This is the leaf evaluation
+ * cit_cfr_pred_fused runs inside its search kernel (model_inference,
+ * deep_mccfr.py:364-374); cit_mlp_forward_wave runs it one row per
+ * workgroup (M workgroups). */
+size_t cit_mlp_wave_bytes(void);
+int cit_mlp_pack_wave(const float* w1t, const float* b1, const float* w2t, const float* b2, const float* w3t,
+                      const float* b3, const float* w4t, const float* b4, void* packed, hipStream_t stream);
+int cit_mlp_forward_wave(const float* feat, int M, const void* packed, float* probs, float* logits,
+                         hipStream_t stream);
 
 /* --- MCCFR (algorithms/deep_mccfr.py) ------------------------------------ */
 
@@ -310,6 +325,19 @@ int cit_cfr_pred_slice(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np
                        int node_cap, int edge_cap, CitOption* optbuf, void* state, const float* probs, float* feat,
                        CitOption* chosen, int64_t slice_ticks, int32_t* waiting, int32_t* running,
                        hipStream_t stream);
+/* cfr_pred(iters, max_depth) + the live choice (run_utils.py:78-81,
+ * deep_mccfr.py:207-229) as ONE launch: every tree runs to its decision
+ * without suspending, evaluating each leaf's encode_game row in its own
+ * kernel with the single-row forward of cit_mlp_forward_wave over
+ * `wave_weights` (cit_mlp_pack_wave).  The trees, streams, chosen[l], root
+ * games and pool are bit-identical to cit_cfr_pred_step's rounds with the
+ * MFMA forward; stats[5*l..] as cit_cfr_decide; state (may be NULL) receives
+ * each tree's final CfrState (phase done).  The pool must be reset with
+ * pred != 0 (a pred-less pool stops each tree with CIT_ERR_UNSUPPORTED). */
+int cit_cfr_pred_fused(void* games, uint32_t* mt, uint32_t* mt_idx, uint32_t* np_mt, uint32_t* np_idx, uint64_t* seer,
+                       int B, int iters, int flags, const int32_t* orig_player, int max_depth, void* pool,
+                       int node_cap, int edge_cap, CitOption* optbuf, const void* wave_weights, void* state,
+                       CitOption* chosen, int32_t* stats, hipStream_t stream);
 
 /* compare_to_random.play_games' step loop (compare_to_random.py:16-35) on
  * every lane up to its next searched decision: seats in search_mask (bit p =

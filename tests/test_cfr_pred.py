@@ -81,3 +81,18 @@ def test_engine_pred_matches_fma_oracle_and_reference(net):
             assert nodes[i]["wp"].tolist() == np.asarray(on.wp, float).tolist()
             if on.pred is not None and nodes[i]["flags"] & 4:
                 assert nodes[i]["pred"].tolist() == np.asarray(on.pred, float).tolist()
+
+
+def test_host_cfr_pred_rejects_pool_without_pred():
+    """The host build of cfr_pred on a pool reset without pred_node_value room
+    stops every tree with CIT_ERR_UNSUPPORTED (the predictions would
+    otherwise overwrite other nodes' rows / edges)."""
+    import numpy as np
+    from hostcheck import HostBatch, HostCfr, cfr_pred
+    hb = HostBatch(list(range(910, 914)), True)
+    cf = HostCfr(hb, node_cap=2048, edge_cap=8192, pred=False)
+    cf.advance(0, 300)
+    calls = []
+    chosen, stats, rounds = cfr_pred(cf, 50, 10, lambda f: calls.append(len(f)) or np.full((len(f), 6), 1 / 6, np.float32))
+    assert rounds == 0 and not calls
+    assert ((stats[:, 4] & 0x40) != 0).all()                  # CIT_ERR_UNSUPPORTED

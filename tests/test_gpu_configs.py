@@ -43,21 +43,44 @@ def _split(t, n):
 
 
 @pytest.mark.timeout(900)
-def test_gpu_config5_200k_queue_golden():
+@pytest.mark.parametrize("rounds", [1, 2], ids=["one_round", "cross_round_queue"])
+def test_gpu_config5_200k_queue_golden(rounds):
+    """rounds = 2: the 64 trees as two data rounds of 32 through one
+    selfplay.TreeQueue (train_from_scratch.collect's cross-round queue: the
+    second round's trees enter the slots the first round's tail frees), each
+    round's result checked as simulate_games' would be."""
     from citadels_self_play_amd import selfplay
     from citadels_self_play_amd.engine import pool_bytes, pool_caps
     recs = {r["seed"]: r for r in load_golden("targets200000.json.gz")}
     seeds = np.arange(CFG5_SEED0, CFG5_SEED0 + CFG5_TREES)
     assert set(recs) <= set(seeds.tolist())
     nc, ec = pool_caps(CFG5_ITERS)
-    budget = pool_bytes(32, nc, ec, selfplay.ARENA_FRAC)       # 32 trees at ARENA_FRAC, overcommitted slots
     msgs = []
     def log(m):                       # progress on stdout (a long test must not look hung)
         msgs.append(m)
         print(m, flush=True)
-    b, stats, t = selfplay.simulate_games(seeds, CFG5_ITERS, max_pool_bytes=budget, log=log)
     tag = "overcommit %.2f" % selfplay.QUEUE_OVERCOMMIT
-    assert selfplay.QUEUE_OVERCOMMIT > 1 and any(tag in m for m in msgs), msgs[-3:]    # the queue ran, overcommitted
+    if rounds == 1:
+        budget = pool_bytes(32, nc, ec, selfplay.ARENA_FRAC)       # 32 trees at ARENA_FRAC, overcommitted slots
+        b, stats, t = selfplay.simulate_games(seeds, CFG5_ITERS, max_pool_bytes=budget, log=log)
+        assert selfplay.QUEUE_OVERCOMMIT > 1 and any(tag in m for m in msgs), msgs[-3:]    # the queue ran, overcommitted
+        _check_cfg5(recs, seeds, b, stats, t)
+        return
+    half = len(seeds) // 2
+    budget = pool_bytes(32, nc, ec, selfplay.ARENA_FRAC)       # a round's 32 trees at ARENA_FRAC
+    q = selfplay.TreeQueue(CFG5_ITERS, half, max_pool_bytes=budget, log=log)
+    q.add(seeds[:half])
+    q.add(seeds[half:])
+    assert q.S == half and q.planner is not None                # both rounds share the slots and arena
+    for r in range(2):
+        q.run(r)
+        b, stats, t = q.result(r)
+        _check_cfg5(recs, seeds[r * half:(r + 1) * half], b, stats, t)
+    q.close()
+    assert any("32 of 32 + " in m for m in msgs), msgs[-3:]        # round 1's trees ran beside round 0's tail
+
+
+def _check_cfg5(recs, seeds, b, stats, t):
     stats_np, chosen = stats.cpu().numpy(), t["chosen"].cpu().numpy()
     per = _split(t, len(seeds))
     counts = t["counts"].cpu().numpy()
@@ -86,7 +109,7 @@ def test_gpu_config5_200k_queue_golden():
         assert hash_obj(mt[:, l].tolist() + [int(idx[l])]) == r["rng_after"][0], s
         assert hash_obj(npmt[:, l].tolist()) == r["rng_after"][1] and int(npidx[l]) == r["rng_after"][2], s
         check_targets(per[l], r["targets"], s)
-    assert n_err >= sum(1 for r in recs.values() if r.get("error"))
+    assert n_err >= sum(1 for r in recs.values() if r.get("error") and r["seed"] in set(seeds.tolist()))
 
 
 def test_gpu_train_from_scratch_on_error(tmp_path):
@@ -127,20 +150,23 @@ def test_gpu_config4_full_size(net, n):
     runs = []
     keep = engine.PRED_SLICE_TICKS
     try:
-        # whole rounds, then 30 us time slices (cit_cfr_pred_slice: many more
-        # search launches), then a strided sub-batch
-        for sel, ticks in ((slice(None), 0), (slice(None), 3000), (slice(3, None, 37), 0)):
+        # in-kernel leaves (one launch, the default); whole leaf rounds, then
+        # 30 us time slices (cit_cfr_pred_slice: many more search launches);
+        # then a strided sub-batch with in-kernel leaves
+        for sel, ticks, fused in ((slice(None), 0, True), (slice(None), 0, False), (slice(None), 3000, False),
+                                  (slice(3, None, 37), 0, True)):
             engine.PRED_SLICE_TICKS = ticks
-            b, chosen, stats, rounds = selfplay.decide(seeds[sel], 200, net=net)
+            b, chosen, stats, rounds = selfplay.decide(seeds[sel], 200, net=net, fused=fused)
             torch.cuda.synchronize()
             runs.append((chosen.cpu().numpy(), stats.cpu().numpy(), b.rows(), b.np_mt.cpu().numpy(),
                          b.mt.cpu().numpy(), rounds, b))
     finally:
         engine.PRED_SLICE_TICKS = keep
-    (c0, s0, r0, n0, m0, k0, b0), (c1, s1, r1, n1, m1, k1, _), (c2, s2, r2, n2, m2, _, _) = runs
-    assert k0 > 10 and k1 >= k0
-    for x, y in ((c0, c1), (s0, s1), (r0, r1), (n0, n1), (m0, m1)):
-        assert np.array_equal(x, y)                                  # deterministic, slice-invariant
+    (c0, s0, r0, n0, m0, k0, b0), (c1, s1, r1, n1, m1, k1, _), (c3, s3, r3, n3, m3, k3, _), \
+        (c2, s2, r2, n2, m2, _, _) = runs
+    assert k0 == 0 and k1 > 10 and k3 >= k1
+    for x, y, z in ((c0, c1, c3), (s0, s1, s3), (r0, r1, r3), (n0, n1, n3), (m0, m1, m3)):
+        assert np.array_equal(x, y) and np.array_equal(x, z)        # mode-, slice-invariant
     for x, y in ((c0[3::37], c2), (s0[3::37, 1:], s2[:, 1:]), (r0[3::37], r2), (n0[:, 3::37], n2), (m0[:, 3::37], m2)):
         assert np.array_equal(x, y)                                  # sub-batch invariant
     assert (s0[:, 4] == 0).mean() > 0.8
@@ -167,7 +193,7 @@ def test_gpu_pred_ahead_invariant(net):
     try:
         for ahead in (1, 4, 8):
             engine.PRED_AHEAD = ahead
-            b, chosen, stats, rounds = selfplay.decide(seeds, 200, net=net)
+            b, chosen, stats, rounds = selfplay.decide(seeds, 200, net=net, fused=False)
             torch.cuda.synchronize()
             runs.append((chosen.cpu().numpy(), stats.cpu().numpy(), b.rows(), b.np_mt.cpu().numpy(),
                          b.np_idx.cpu().numpy(), b.mt.cpu().numpy(), b.mt_idx.cpu().numpy(), rounds))

@@ -1,13 +1,14 @@
 """Featurizers, value MLP and model-driven MCCFR on a real MI355X through the
 C ABI (cit_encode_games / cit_encode_options / cit_mlp_forward /
-cit_cfr_pred_step).
+cit_mlp_forward_wave / cit_cfr_pred_step / cit_cfr_pred_fused).
 
 * encode kernels == the host build of the same headers (itself pinned to the
   reference's encodings, test_encode_host_golden.py), bit for bit;
-* the fp32-MFMA MLP == the fmaf-chain oracle (oracle/mlp_fma.c) bit for bit,
-  and within PROB_RTOL/PROB_ATOL of the reference's own forward (mlp.npz);
-* cfr_pred(200, 10) with the seeded value net: trees == the oracle driven by
-  the fmaf-chain MLP bit for bit; node/carry_out counts, root game and
+* the fp32-MFMA MLP and the single-row wave MLP == the fmaf-chain oracle
+  (oracle/mlp_fma.c) bit for bit, and within PROB_RTOL/PROB_ATOL of the
+  reference's own forward (mlp.npz);
+* cfr_pred(200, 10) with the seeded value net, leaves in the search kernel
+  and in leaf rounds: trees == the oracle driven by the fmaf-chain MLP bit for bit; node/carry_out counts, root game and
   decisions == the reference (cfr_pred200), root values within VALUE_ATOL."""
 import numpy as np
 import pytest
@@ -67,6 +68,25 @@ def test_gpu_mlp_layer_split_equals_fused(golden, rows):
     assert np.array_equal(pa[:k].cpu().numpy().view(np.uint32), fp.view(np.uint32))
 
 
+@pytest.mark.parametrize("variant", ["init", "bn"])
+def test_gpu_mlp_wave_bitwise_vs_fma_oracle(golden, variant):
+    """The single-row forward the search kernel evaluates its leaves with
+    (cit_mlp_forward_wave: one row per wavefront, VALU fmaf chains over the wave
+    layout) == the fmaf-chain oracle == the MFMA layer-split path, bit for bit."""
+    m = load_variant(golden, variant)
+    net = models.ValueNet(m, "cuda")
+    x = np.concatenate([golden["x"], golden["x"][:45] * 0.5, -golden["x"][:19] * 3.0])
+    xd = torch.from_numpy(x).cuda()
+    probs, logits = net.forward(xd, logits=True, wave=True)
+    pk, lk = net.forward(xd, logits=True)
+    probs, logits = probs.cpu().numpy(), logits.cpu().numpy()
+    fp, fl = M.FmaMLP(models.fold(m))(x, logits=True)
+    assert np.array_equal(logits.view(np.uint32), fl.view(np.uint32))
+    assert np.array_equal(probs.view(np.uint32), fp.view(np.uint32))
+    assert np.array_equal(lk.cpu().numpy().view(np.uint32), logits.view(np.uint32))
+    assert np.array_equal(pk.cpu().numpy().view(np.uint32), probs.view(np.uint32))
+
+
 def test_gpu_mlp_packed_rejects_short_workspace(golden):
     from citadels_self_play_amd import _lib
     net = models.ValueNet(load_variant(golden, "init"), "cuda")
@@ -112,7 +132,11 @@ def test_gpu_encode_matches_host():
         i += k
 
 
-def test_gpu_cfr_pred_golden(golden):
+@pytest.mark.parametrize("fused", [True, False], ids=["in_kernel_leaves", "leaf_rounds"])
+def test_gpu_cfr_pred_golden(golden, fused):
+    """Both cfr_pred modes: leaves evaluated inside the search kernel
+    (cit_cfr_pred_fused, the default) and rounds of search launches + MFMA
+    leaf launches (cit_cfr_pred_slice)."""
     from citadels_self_play_amd.engine import GameBatch
     m = load_variant(golden, "bn")
     net = models.ValueNet(m, "cuda")
@@ -121,9 +145,9 @@ def test_gpu_cfr_pred_golden(golden):
     b = GameBatch([r["seed"] for r in recs], preset=True)
     b.advance_random(0, 300)
     b.seed_numpy()
-    chosen, stats, rounds = b.cfr_pred(200, net, max_depth=10, node_cap=2048)
+    chosen, stats, rounds = b.cfr_pred(200, net, max_depth=10, node_cap=2048, fused=fused)
     torch.cuda.synchronize()
-    assert rounds > 10
+    assert rounds > 10 if not fused else rounds == 0
     chosen, stats, rows = chosen.cpu().numpy(), stats.numpy(), b.rows()
     for l, r in enumerate(recs):
         root, n_nodes, n_edges, carry, err = stats[l]
@@ -144,3 +168,59 @@ def test_gpu_cfr_pred_golden(golden):
         assert len(order) == len(onodes), r["seed"]
         for i, on in zip(order, onodes):
             assert nodes[i]["nv"].tolist() == np.asarray(on.nv, float).tolist(), r["seed"]
+
+
+def test_gpu_cfr_pred_rejects_pool_without_pred(golden):
+    """A pool reset without pred_node_value room (cit_cfr_arena_reset_fmt pred=0)
+    stops every cfr_pred tree with CIT_ERR_UNSUPPORTED instead of writing the
+    predictions over other records (both the fused and the resumable kernels)."""
+    from citadels_self_play_amd import _lib
+    from citadels_self_play_amd.engine import GameBatch
+    net = models.ValueNet(load_variant(golden, "bn"), "cuda")
+    lib = _lib.load()
+    b = GameBatch(list(range(900, 908)), preset=True)
+    b.advance_random(0, 300)
+    b.seed_numpy()
+    for fused in (True, False):
+        b._pool(2048, 4 * 2048, pred=False)
+        B = b.B
+        state = torch.zeros((B, lib.cit_cfr_state_bytes() // 4), dtype=torch.int32, device="cuda")
+        chosen = torch.zeros((B, 16), dtype=torch.uint8, device="cuda")
+        p = lambda t: t.data_ptr()
+        args = (p(b.games), p(b.mt), p(b.mt_idx), p(b.np_mt), p(b.np_idx), p(b.seer), B, 200, 0, None, 10,
+                p(b.pool), b.node_cap, b.edge_cap, p(b.optbuf))
+        if fused:
+            stats = torch.zeros((B, 5), dtype=torch.int32, device="cuda")
+            _lib.check(lib.cit_cfr_pred_fused(*args, net.wave.data_ptr(), p(state), p(chosen), p(stats), None), "fused")
+            err = stats[:, 4].cpu().numpy()
+        else:
+            probs = torch.zeros((B, 6), dtype=torch.float32, device="cuda")
+            feat = torch.zeros((B, 418), dtype=torch.float32, device="cuda")
+            waiting = torch.zeros(2, dtype=torch.int32, device="cuda")
+            _lib.check(lib.cit_cfr_pred_step(*args, p(state), p(probs), p(feat), p(chosen), p(waiting), None), "step")
+            assert int(waiting[0]) == 0
+            err = state[:, 2].cpu().numpy()
+        torch.cuda.synchronize()
+        assert (err & 0x40).all(), (fused, err)          # CIT_ERR_UNSUPPORTED
+
+
+def test_gpu_mlp_wave_nonfinite_weight_reads_every_row(golden):
+    """A non-finite weight clears the wave layout's flag word (0 * inf is NaN,
+    not a no-op), so the single-row forward reads every input row and still
+    equals the MFMA path, NaNs and infinities included."""
+    m = load_variant(golden, "bn")
+    net = models.ValueNet(m, "cuda")
+    flag = int(net.wave.view(torch.int32)[-4])           # MLPW_FLAG (then 3 pad words)
+    assert flag == 1                                         # finite weights: zero inputs skipped
+    with torch.no_grad():
+        m.fc3.weight[0, 5] = float("inf")
+        m.fc2.weight[3, 7] = float("-inf")
+    net = models.ValueNet(m, "cuda")
+    assert int(net.wave.view(torch.int32)[-4]) == 0
+    x = torch.from_numpy(np.concatenate([golden["x"], golden["x"][:45] * 0.5])).cuda()
+    pw, lw = net.forward(x, logits=True, wave=True)
+    pk, lk = net.forward(x, logits=True)
+    pw, lw, pk, lk = (t.cpu().numpy() for t in (pw, lw, pk, lk))
+    assert not np.isfinite(lk).all()                         # the infinities reach the logits somewhere
+    np.testing.assert_array_equal(lw, lk)                    # (NaN == NaN here)
+    np.testing.assert_array_equal(pw, pk)

@@ -3,7 +3,10 @@
 ~20 µs .. 5 ms equal simulate_games' one launch bit for bit -- stats, targets
 in seed order, final games and both streams -- also when small node caps make
 trees overflow or the shared arena runs out and trees go through the
-cfr_decide retry."""
+cfr_decide retry.  The cross-round queue (selfplay.TreeQueue: rounds of
+positions back to back, later rounds' trees taking the slots an earlier
+round's tail frees, rounds added while the queue runs) gives each round
+exactly simulate_games' result for its seeds."""
 import pytest
 import torch
 
@@ -64,3 +67,30 @@ def test_gpu_queue_overcommit_pauses(overcommit, frac):
                                 log=msgs.append)
     _same(q, whole)
     assert any("tree-slices paused" in m for m in msgs)
+
+
+@pytest.mark.parametrize("overcommit,frac", [(None, "auto"), (2.5, (0.3, 0.5))])
+def test_gpu_tree_queue_rounds_match_batches(overcommit, frac):
+    from citadels_self_play_amd import selfplay
+    rounds = [selfplay.shard(10, 9190 + 100 * r, 0, 1) for r in range(3)]
+    whole = [selfplay.simulate_games(sd, 2000) for sd in rounds]
+    q = selfplay.TreeQueue(2000, 10, slots=4, slice_seconds=2e-3, overcommit=overcommit, arena_frac=frac)
+    q.add(rounds[0])
+    q.add(rounds[1])
+    added = []
+
+    def more(qq):                 # round 2 added from the slice callback once round 1's trees run
+        if len(qq.rounds) == 2 and qq.rounds[1].n_done >= 1:
+            added.append(qq.add(rounds[2]))
+    got = []
+    for r in range(3):
+        q.run(r, on_slice=more)
+        if len(q.rounds) == 2:    # (round 1 may have finished inside run(0))
+            q.add(rounds[2])
+        got.append(q.result(r))
+        walked, n = q.targets_so_far(r)
+        assert walked == 10 and n == int(got[-1][2]["counts"][:, 0].sum())
+    q.close()
+    assert len(q.rounds) == 3 and added in ([], [2])
+    for a, b in zip(got, whole):
+        _same(a, b)

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--node-cap", type=int, default=1024)
     ap.add_argument("--pred", action="store_true")
+    ap.add_argument("--fused", type=int, default=-1, help="config 4: 1 in-kernel leaves, 0 leaf rounds, -1 default")
     a = ap.parse_args()
     net = None
     if a.pred:
@@ -44,14 +45,15 @@ def main():
         if net is None:
             chosen, stats = b.cfr_decide(a.iters, node_cap=a.node_cap)
         else:
-            chosen, stats, rounds = b.cfr_pred(a.iters, net, max_depth=10, node_cap=a.node_cap)
+            chosen, stats, rounds = b.cfr_pred(a.iters, net, max_depth=10, node_cap=a.node_cap,
+                                               fused="auto" if a.fused < 0 else bool(a.fused))
         e1.record()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         ms = e0.elapsed_time(e1)
         st = stats.cpu().numpy()
         ok = st[:, 4] == 0
-        print(json.dumps({"config": "config4" if net else "config3", "rounds": rounds, "B": a.batch, "iters": a.iters, "kernel_ms": ms, "wall_s": wall,
+        print(json.dumps({"config": "config4" if net else "config3", "fused": a.fused, "rounds": rounds, "B": a.batch, "iters": a.iters, "kernel_ms": ms, "wall_s": wall,
                           "decisions_per_s": a.batch / (ms * 1e-3),
                           "carry_out_per_s": float(st[:, 3].sum()) / (ms * 1e-3),
                           "nodes_mean": float(st[:, 1].mean()), "nodes_max": int(st[:, 1].max()),

@@ -46,8 +46,14 @@ def run(lib_path=LIB):
     from citadels_self_play_amd.engine import GameBatch, pool_caps
     lib = _lib.load()
     lib.cit_tree_clock_read.argtypes = [C.c_void_p, C.c_int]
-    for tag, B, iters, rep in (("config3", 1024, 200, 0), ("config3", 1024, 200, 1), ("config3", 1024, 200, 2),
-                               ("config5_2000", 1024, 2000, 0)):
+    loads = (("config3", 1024, 200, 0), ("config3", 1024, 200, 1), ("config3", 1024, 200, 2),
+             ("config5_2000", 1024, 2000, 0), ("config4", 512, 200, 0), ("config4", 512, 200, 1),
+             ("config4", 4096, 200, 0), ("config4", 4096, 200, 1))
+    only = os.environ.get("TREE_CLOCK_ONLY")          # e.g. "config4": those workloads only
+    net = None
+    for tag, B, iters, rep in loads:
+        if only and tag not in only.split(","):
+            continue
         seeds = selfplay.shard(B, base_seed=30_000_000 + rep * B)
         b = GameBatch(seeds, preset=True)
         if iters == 200:
@@ -56,10 +62,17 @@ def run(lib_path=LIB):
             b.random_position(100)
         b.seed_numpy()
         nc, ec = pool_caps(iters)
+        if tag == "config4" and net is None:
+            from citadels_self_play_amd import models
+            torch.manual_seed(0)
+            net = models.ValueNet(models.ValueOnlyNN(418, 512), "cuda")
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        chosen, stats = b._cfr_decide(iters, nc, ec)
+        if tag == "config4":           # cfr_pred with in-kernel leaves (k_cfr_pred_fused keeps the same clock)
+            chosen, stats, _ = b.cfr_pred(iters, net, max_depth=10, node_cap=4096, fused=True)
+        else:
+            chosen, stats = b._cfr_decide(iters, nc, ec)
         e1.record()
         torch.cuda.synchronize()
         buf = (C.c_ulonglong * (2 * B))()

@@ -33,9 +33,9 @@ OUT = os.path.join(ROOT, "build", "cfrprof")
 NAMES = ["carry", "prepare", "list_lds", "pick", "list", "sample", "copy_row", "cfr_node", "exp_role", "exp_own",
          "exp_opp", "upd_strategy", "choose", "upd_regrets", "backprop", "live_choice",
          "smp_used", "smp_unknown", "smp_deck", "smp_warrants", "smp_opponents", "skip_false", "row_store",
-         "row_load"] + ["s%d" % i for i in range(24, 32)]
+         "row_load", "leaf_eval"] + ["s%d" % i for i in range(25, 32)]
 VARIANTS = {"top": (8, 9, 10, 11, 12, 14, 15), "node": (5, 6, 7), "engine": (0, 1, 2, 3, 4),
-            "sample": (5, 16, 17, 18, 19, 20), "rows": (7, 21, 22, 23)}
+            "sample": (5, 16, 17, 18, 19, 20), "rows": (7, 21, 22, 23), "pred": (8, 9, 10, 11, 12, 14, 24)}
 
 
 def lib_of(name):
@@ -55,7 +55,10 @@ def build():
         print(lib_of(name))
 
 
-def _workload(GameBatch, pool_caps, torch, B, iters):
+_NET = []
+
+
+def _workload(GameBatch, pool_caps, torch, B, iters, pred=False):
     b = GameBatch(np.arange(20_000_000, 20_000_000 + B), preset=True)
     if iters <= 200:
         b.advance_random(0, 300)
@@ -66,8 +69,15 @@ def _workload(GameBatch, pool_caps, torch, B, iters):
     nc, ec = pool_caps(iters)
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
+    if pred and not _NET:
+        from citadels_self_play_amd import models
+        torch.manual_seed(0)
+        _NET.append(models.ValueNet(models.ValueOnlyNN(418, 512), "cuda"))
     t0.record()
-    chosen, stats = b._cfr_decide(iters, nc, ec)
+    if pred:               # config 4: cfr_pred(iters, 10) with in-kernel leaves
+        chosen, stats, _ = b.cfr_pred(iters, _NET[0], max_depth=10, node_cap=4096, fused=True)
+    else:
+        chosen, stats = b._cfr_decide(iters, nc, ec)
     t1.record()
     torch.cuda.synchronize()
     return t0.elapsed_time(t1), stats.cpu().numpy()
@@ -87,12 +97,14 @@ def run(which=None, workloads=None):
         if vname != "plain":
             lib.cit_prof_read.argtypes = [C.c_void_p]
             buf = (C.c_ulonglong * 64)()
-        wl = (("config3", 1024, 200), ("config5_2000", 1024, 2000)) if not workloads else \
-            [("iters%s_b%s" % tuple(w.split(":")), int(w.split(":")[1]), int(w.split(":")[0])) for w in workloads.split(",")]
-        for tag, B, iters in wl:
+        # workloads "ITERS:B" (cfr_train) or "pred:ITERS:B" (cfr_pred, config 4)
+        wl = (("config3", 1024, 200, False), ("config5_2000", 1024, 2000, False)) if not workloads else \
+            [("%s_b%s" % (w.rsplit(":", 1)[0].replace(":", ""), w.rsplit(":", 1)[1]), int(w.rsplit(":", 1)[1]),
+              int(w.split(":")[-2]), w.startswith("pred:")) for w in workloads.split(",")]
+        for tag, B, iters, pred in wl:
             if vname != "plain":
                 lib.cit_prof_read(buf)
-            ms, st = _workload(GameBatch, pool_caps, torch, B, iters)
+            ms, st = _workload(GameBatch, pool_caps, torch, B, iters, pred)
             if vname == "plain":
                 plain[tag] = ms
                 continue
@@ -109,4 +121,5 @@ def run(which=None, workloads=None):
 
 
 if __name__ == "__main__":
-    build() if sys.argv[1:] == ["build"] else run(*sys.argv[2:])   # run [variant] [iters:B,...]
+    # run [variant] [iters:B ...]  (workloads comma- or space-separated)
+    build() if sys.argv[1:] == ["build"] else run(*(sys.argv[2:3] + ([",".join(sys.argv[3:])] if sys.argv[3:] else [])))

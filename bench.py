@@ -93,7 +93,7 @@ N_CU, CLOCK_HZ, SIMD_PER_CU = 256, 2.4e9, 4
 SALU_PEAK = N_CU * CLOCK_HZ  # one scalar instruction per clock per CU
 BASE_SEED = 1_000_000_000
 CFR_SEED = 30_000_000        # configs 3-5: positions / trees seeded from here (tools/bench_selfplay.py)
-KERNELS = {2: "k_rollout_u", 3: "k_cfr_decide", 4: "k_cfr_pred_step", 5: "k_cfr_train_slice"}
+KERNELS = {2: "k_rollout_u", 3: "k_cfr_decide", 4: "k_cfr_pred_fused", 5: "k_cfr_train_slice"}
 # The reference's own Python, BASELINE.md §2 config 1 (survey container, 8-core Xeon).
 REF_PY = {"1_core": 12301, "8_procs": 83869, "unit": "carry_out transitions/s",
           "where": "survey container (BASELINE.md), not this box"}
@@ -249,28 +249,39 @@ def _pmc_pass(counters, outdir, config=2, timeout_s=150, cfr_child=False):
         raise RuntimeError("rocprofv3 --pmc %s exited %d" % (counters, rc))
     rows = _rows(os.path.join(outdir, "**", "*counter_collection.csv"))
     if cfr_child:
-        out = {}
-        # the child runs configs 3, 4, 5 in that order: config 3's k_cfr_decide
-        # dispatches precede config 4's first (config 5's overflow retries, if
-        # any, also launch k_cfr_decide: they come after)
-        c4 = [int(r["Dispatch_Id"]) for r in rows if KERNELS[4] in r.get("Kernel_Name", "") and "Dispatch_Id" in r]
-        first4 = min(c4) if c4 else None
-        for kernel in (KERNELS[3], KERNELS[4], KERNELS[5]):
-            per = {}
-            for r in rows:
-                if kernel == KERNELS[3] and first4 is not None and int(r.get("Dispatch_Id", "0")) > first4:
-                    continue
-                if kernel in r.get("Kernel_Name", ""):
-                    per.setdefault(r["Counter_Name"], {}).setdefault(r.get("Dispatch_Id", "0"), 0.0)
-                    per[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
-            if per:
-                out[kernel] = {k: sum(v.values()) for k, v in per.items()}
-                out[kernel]["_launches"] = max(len(v) for v in per.values())
         with open(logp) as f:
             lines = [ln for ln in f if ln.startswith("{\"pmc_child\"")]
-        if not out or not lines:
-            raise RuntimeError("no search-kernel rows / child line in the rocprofv3 output")
-        out["_child"] = json.loads(lines[-1])
+        if not lines:
+            raise RuntimeError("no child line in the rocprofv3 output")
+        child = json.loads(lines[-1])
+        # the child runs PMC_CHILD_LEGS in order and reports each leg's launches
+        # of its search kernel: a kernel's dispatches, in dispatch order, go to
+        # those legs in turn (later dispatches -- e.g. config 5's overflow
+        # retries, which launch k_cfr_decide -- to none)
+        per_kernel = {}
+        for r in rows:
+            k = next((k for k in set(KERNELS.values()) if k in r.get("Kernel_Name", "")), None)
+            if k is not None and "Dispatch_Id" in r:
+                d = per_kernel.setdefault(k, {}).setdefault(int(r["Dispatch_Id"]), {})
+                d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        taken = {k: 0 for k in per_kernel}
+        out = {}
+        for key, c, _ in PMC_CHILD_LEGS:
+            k = KERNELS[c]
+            ids = sorted(per_kernel.get(k, {}))
+            n = int(child[key]["launches"])
+            mine = ids[taken.get(k, 0):taken.get(k, 0) + n]
+            taken[k] = taken.get(k, 0) + n
+            tot = {}
+            for i in mine:
+                for name, v in per_kernel[k][i].items():
+                    tot[name] = tot.get(name, 0.0) + v
+            if tot:
+                tot["_launches"] = len(mine)
+                out[key] = tot
+        if not out:
+            raise RuntimeError("no search-kernel rows in the rocprofv3 output")
+        out["_child"] = child
         return out
     kernel = KERNELS[config]
     per = {}
@@ -283,6 +294,41 @@ def _pmc_pass(counters, outdir, config=2, timeout_s=150, cfr_child=False):
     out = {k: sum(v.values()) / len(v) for k, v in per.items()}
     out["_launches"] = max(len(v) for v in per.values())
     return out
+
+
+def trace_in_run(args, timeout_s=300):
+    """rocprofv3 --kernel-trace --stats over a child run of this script's
+    config-2 workload with every launch alone (--streams 1, the same --steps /
+    --warmup): {calls, avg_ms, min_ms, max_ms} of k_rollout_u and the stats
+    CSV's path.  The roofline is priced on this duration (the profiler's
+    kernel begin / end), not on HIP events around the launch."""
+    outdir = tempfile.mkdtemp(prefix="bench_trace_", dir="/tmp")
+    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-pmc", "--no-cfr",
+             "--config", "2", "--streams", "1", "--steps", str(args.steps), "--warmup", str(args.warmup),
+             "--batch", str(args.batch)]
+    cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", outdir, "-o", "run", "--"] + child
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        with open(os.path.join(outdir, "log.txt"), "w") as log:
+            p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+            try:
+                rc = p.wait(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                raise RuntimeError("rocprofv3 --kernel-trace timed out")
+        if rc != 0:
+            raise RuntimeError("rocprofv3 --kernel-trace exited %d" % rc)
+        paths = glob.glob(os.path.join(outdir, "**", "*kernel_stats.csv"), recursive=True)
+        rows = _rows(os.path.join(outdir, "**", "*kernel_stats.csv"))
+        row = next(r for r in rows if KERNELS[2] in r["Name"])
+        return {"calls": int(row["Calls"]), "avg_ms": float(row["AverageNs"]) * 1e-6,
+                "min_ms": float(row["MinNs"]) * 1e-6, "max_ms": float(row["MaxNs"]) * 1e-6,
+                "stats_csv": paths[0] if paths else None,
+                "command": "rocprofv3 --kernel-trace --stats -- python bench.py --config 2 --streams 1 --steps %d "
+                           "--warmup %d --no-cfr --no-pmc --no-cpu-baseline" % (args.steps, args.warmup)}
+    except Exception as e:  # a missing profiler must not cost the bench line
+        return {"error": str(e)[:300]}
 
 
 def pmc_in_run(config=2):
@@ -305,15 +351,16 @@ def pmc_in_run(config=2):
 # Counter passes over one --pmc-child run of the three search workloads (their
 # kernels are distinct, so one child serves configs 3, 4 and 5).
 CFR_PMC_PASSES = (["FETCH_SIZE"], ["WRITE_SIZE"], SQ_SET, ["SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"])
-# positions / trees per config in the --pmc-child run.  Config 5 runs at its
-# bench size: fewer trees fit in HBM at once and would search in k_cfr_decide
-# (simulate_games without the queue), not in the queue's k_cfr_train_slice.
-PMC_CHILD = {3: 1024, 4: 4096, 5: 1920}
+# The --pmc-child run's legs, in order: (key, config, positions / trees).  Config 5
+# runs at its bench size: fewer trees fit in HBM at once and would search in
+# k_cfr_decide (simulate_games without the queue), not in the queue's
+# k_cfr_train_slice.  "4@512" is config 4's per-rank shard of the 8-GPU job.
+PMC_CHILD_LEGS = (("3", 3, 1024), ("4@512", 4, 512), ("4", 4, 4096), ("5", 5, 1920))
 
 
 def pmc_in_run_cfr():
-    """Four --pmc passes over `bench.py --pmc-child` (configs 3, 4, 5 once each
-    at PMC_CHILD sizes, no warm-up).  Returns {config: {counter: total,
+    """Four --pmc passes over `bench.py --pmc-child` (PMC_CHILD_LEGS once each,
+    no warm-up).  Returns {leg key: {counter: total over the leg's launches,
     "carry_outs": the child's carry_outs, "search_ms": its search time}}."""
     base = tempfile.mkdtemp(prefix="bench_pmc_cfr_", dir="/tmp")
     out = {}
@@ -321,15 +368,14 @@ def pmc_in_run_cfr():
         for i, ctrs in enumerate(CFR_PMC_PASSES):
             r = _pmc_pass(ctrs, os.path.join(base, "p%d" % i), cfr_child=True, timeout_s=240)
             child = r.pop("_child")
-            for c in (3, 4, 5):
-                k = KERNELS[c]
-                d = out.setdefault(c, {"kernel": k, "source": "in-run rocprofv3 --pmc, %d passes over one "
-                                       "`bench.py --pmc-child` run (%d %s)" % (len(CFR_PMC_PASSES), PMC_CHILD[c],
-                                                                         "trees" if c == 5 else "positions")})
-                d.update(r.get(k, {}))
-                d["carry_outs_pass%d" % i] = child[str(c)]["carry_outs"]
-                d["search_ms_pass%d" % i] = child[str(c)]["search_ms"]
-                d["carry_outs"] = child[str(c)]["carry_outs"]
+            for key, c, n in PMC_CHILD_LEGS:
+                d = out.setdefault(key, {"kernel": KERNELS[c], "source": "in-run rocprofv3 --pmc, %d passes over one "
+                                         "`bench.py --pmc-child` run (%d %s)" % (len(CFR_PMC_PASSES), n,
+                                                                           "trees" if c == 5 else "positions")})
+                d.update(r.get(key, {}))
+                d["carry_outs_pass%d" % i] = child[key]["carry_outs"]
+                d["search_ms_pass%d" % i] = child[key]["search_ms"]
+                d["carry_outs"] = child[key]["carry_outs"]
     except Exception as e:  # a missing profiler must not cost the bench line
         out["error"] = str(e)[:300]
     return out
@@ -512,7 +558,10 @@ def run_rollout(args, world, rank, dev, n_dev, pmc):
     if rank != 0:
         return None
     per_launch_trans = trans_s / K
-    avg_ms = float(np.mean(kernel_ms))
+    events_ms = float(np.mean(kernel_ms))
+    trace = (pmc or {}).get("trace") or {}
+    # the kernel's own duration from the in-run kernel trace (every launch alone); HIP events otherwise
+    avg_ms = trace["avg_ms"] if trace.get("avg_ms") else events_ms
     alg_bytes = per_launch_trans * 2 * L.GAME_BYTES
     hbm_achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
@@ -531,6 +580,12 @@ def run_rollout(args, world, rank, dev, n_dev, pmc):
     roof.update({
         "traffic": traffic, "kernel": KERNELS[2] if args.games_per_block <= 0 else "k_rollout (lanes)",
         "kernel_avg_ms": avg_ms, "launches": K,
+        "kernel_avg_ms_source": "rocprofv3 --kernel-trace (in-run child, %d launches alone)" % trace["calls"]
+        if trace.get("avg_ms") else "HIP events around each launch (one stream)",
+        "kernel_avg_ms_events": events_ms, "trace": trace or None,
+        "timed_mode": {"ms_per_step": elapsed / K * 1e3, "streams": S,
+                       "hbm_notional_gbs": per_launch_trans * 2 * L.GAME_BYTES / (elapsed / K) / 1e9,
+                       "note": "the headline's own clock: K launches on S streams overlapping, per step"},
         "wait_any_frac": issue.get("wait_any_frac") if issue else None, "busy_frac": busy,
         "hbm_notional": hbm_notional,
         "measured_gbs": (traffic / (avg_ms * 1e-3) / 1e9) if traffic else None,
@@ -889,15 +944,20 @@ def main():
         torch.cuda.set_device(dev)
         args.cfr_streams = 1
         line = {"pmc_child": 1}
-        for c in (3, 4, 5):
-            r = run_cfr(c, args, 1, 0, dev, cpu=False, per_gpu=PMC_CHILD[c], warm_rep=False, n_reps=1)
+        from citadels_self_play_amd import engine
+        for key, c, n in PMC_CHILD_LEGS:
+            before = engine.LAUNCHES.get(KERNELS[c], 0)
+            r = run_cfr(c, args, 1, 0, dev, cpu=False, per_gpu=n, warm_rep=False, n_reps=1)
             m = r["median"]
-            line[str(c)] = {"carry_outs": m["carry_out_per_s"] * m["seconds"], "search_ms": m["seconds"] * 1e3}
+            line[key] = {"carry_outs": m["carry_out_per_s"] * m["seconds"], "search_ms": m["seconds"] * 1e3,
+                         "launches": engine.LAUNCHES.get(KERNELS[c], 0) - before}
         print(json.dumps(line), flush=True)
         return
 
     # The PMC passes run as child processes before this process touches the GPU.
     pmc = pmc_in_run(2) if (args.config == 2 and world == 1 and not args.no_pmc) else None
+    if pmc is not None:
+        pmc["trace"] = trace_in_run(args)
     cfr_pmc = pmc_in_run_cfr() if (world == 1 and not args.no_pmc and (cfr_list or args.config != 2)) else {}
 
     dev = torch.device("cuda", local % max(1, n_dev))
@@ -909,7 +969,7 @@ def main():
     if args.config == 2:
         out = run_rollout(args, world, rank, dev, n_dev, pmc)
     else:
-        c = run_cfr(args.config, args, world, rank, dev, pmc=cfr_pmc.get(args.config))
+        c = run_cfr(args.config, args, world, rank, dev, pmc=cfr_pmc.get(str(args.config)))
         out = None
         if rank == 0:
             out = {"metric": "MCCFR config %d" % args.config, "value": c["value"], "unit": c["unit"],
@@ -923,7 +983,7 @@ def main():
         try:
             c, _, n = key.partition("@")
             c = int(c)
-            r = run_cfr(c, args, world, rank, dev, pmc=None if n else cfr_pmc.get(c), per_gpu=int(n) if n else None,
+            r = run_cfr(c, args, world, rank, dev, pmc=cfr_pmc.get(key), per_gpu=int(n) if n else None,
                         cpu=not n)
             if n and r is not None:
                 r["shard_of"] = {4: "config 4's 4096 positions over 8 GPUs (the per-rank work of that config)",

@@ -1657,13 +1657,14 @@ CIT_NOINLINE void cfr_leaf_eval(CfrTree& T_in, int n, const float* wave_w) {
   for (int i = CFR_LANE; i < MLPW_IN + 2; i += CFR_TEAM) R[MLPW_R_X + i] = 0.0f;
   CFR_SYNC();
   float* x = (float*)(R + MLPW_R_X);
-  if (cfr_u(T.row_cap) == 0) {
-    cit_encode_game<float, false>(*reinterpret_cast<const CitGame*>(row_of(T, n)), x, pid);
-  } else {
+  // the node's row into w0 first (one round of loads): the featurizer's field
+  // reads are then LDS reads, not a chain of dependent HBM loads
+  if (cfr_u(T.row_cap) == 0)
+    copy_row(T, w_row(T, 0), row_of(T, n));
+  else
     row_load(T, w_row(T, 0), n);
-    CFR_SYNC();
-    cit_encode_game<float, false>(cfr_w(T, 0), x, pid);
-  }
+  CFR_SYNC();
+  cit_encode_game<float, false>(cfr_w(T, 0), x, pid);
   mlpw_forward(wave_w, R);
   cfr_ls.cnode = -1;
 }

@@ -59,19 +59,15 @@ MLPW_HD constexpr long mlpw_floats(int K, int N) { return (long)K * mlpw_rs(N); 
 #define MLPW_TOTAL (MLPW_FLAG + 4)
 
 // The forward's LDS scratch (floats): h1 [0, 512) | x [512, 932) (418 + two
-// zero pads) | layer 1's list of non-zero inputs (int16) from 936 -- layer 1
-// reads x and writes h1 --; then h2 over x with layer 2's list at [768, 1024),
-// h3 over h1, layers 3 / 4's lists at 768, and the logits / probabilities at
-// [1024, 1040).
+// zero pads) -- layer 1 reads x and writes h1 --, then h2 over x, h3 over h1,
+// and the logits / probabilities at [768, 780).
 #define MLPW_R_H1 0
 #define MLPW_R_X 512
-#define MLPW_R_L1 936
 #define MLPW_R_H2 512
-#define MLPW_R_LN 768
 #define MLPW_R_H3 0
-#define MLPW_R_LOGITS 1024
-#define MLPW_R_PROBS 1032
-#define MLPW_R_FLOATS 1146
+#define MLPW_R_LOGITS 768
+#define MLPW_R_PROBS 776
+#define MLPW_R_FLOATS 932
 
 // Element e of the row layout of W [K][N] (row-major, k major).
 MLPW_HD inline float mlpw_pack_elem(const float* W, int K, int N, long e) {
@@ -87,7 +83,6 @@ MLPW_HD inline float mlpw_pack_elem(const float* W, int K, int N, long e) {
 
 #if defined(__HIPCC__)
 typedef __attribute__((address_space(3))) float mlpw_lds_t;
-typedef __attribute__((address_space(3))) int16_t mlpw_lds_i16;
 typedef float mlpw_f4 __attribute__((ext_vector_type(4)));
 typedef float mlpw_f2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) float mlpw_gf_t;
@@ -100,21 +95,53 @@ __device__ __forceinline__ mlpw_gf_t* mlpw_glb(const float* p) {
   return (mlpw_gf_t*)(((uint64_t)hi << 32) | lo);
 }
 
-// The ascending list of input indices k < K whose x[k] is non-zero (every k
-// when !skip) into `list`; returns its length (wave-uniform).
+// The non-zero inputs of a layer as 64-bit masks, one per 64 inputs (every
+// input when !skip), held in two VGPRs (lane i: chunk i's mask) so a scalar
+// cursor walks the set bits in ascending order with readlane / ctz -- no LDS
+// list, so the next row's address is a few scalar instructions away.
+struct MlpwMask {
+  uint32_t lo, hi;      // lane i: bits of chunk i (per lane: a VGPR)
+  int nnz;              // set bits in all (wave-uniform)
+};
 template <int K>
-__device__ __forceinline__ int mlpw_list(const mlpw_lds_t* x, mlpw_lds_i16* list, bool skip) {
+__device__ __forceinline__ MlpwMask mlpw_mask(const mlpw_lds_t* x, bool skip) {
   const int lane = __lane_id();
-  int n = 0;
+  MlpwMask M{0u, 0u, 0};
 #pragma unroll
   for (int i = 0; i < K; i += 64) {
     const int k = i + lane;
     const bool nz = k < K && (!skip || x[k < K ? k : 0] != 0.0f);
     const uint64_t m = __ballot(nz);
-    if (nz) list[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = (int16_t)k;
-    n += __popcll(m);
+    if (lane == i / 64) {
+      M.lo = (uint32_t)m;
+      M.hi = (uint32_t)(m >> 32);
+    }
+    M.nnz += __popcll(m);
   }
-  return __builtin_amdgcn_readfirstlane(n);
+  M.nnz = __builtin_amdgcn_readfirstlane(M.nnz);
+  return M;
+}
+// A cursor over the set bits of a MlpwMask (scalar state).
+struct MlpwCursor {
+  int ci;               // current chunk
+  uint64_t cm;          // its bits not yet taken
+};
+__device__ __forceinline__ uint64_t mlpw_chunk(const MlpwMask& M, int ci) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)M.hi, ci) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)M.lo, ci);
+}
+// The next set input index (0 past the end: a dummy row, never consumed).
+template <int K>
+__device__ __forceinline__ int mlpw_next(const MlpwMask& M, MlpwCursor& c) {
+  constexpr int NCH = (K + 63) / 64;
+  while (c.cm == 0 && c.ci < NCH - 1) {
+    c.ci++;
+    c.cm = mlpw_chunk(M, c.ci);
+  }
+  if (c.cm == 0) return 0;
+  const int b = __builtin_ctzll(c.cm);
+  c.cm &= c.cm - 1;
+  return 64 * c.ci + b;
 }
 
 // S floats of weight row k for this lane (S = 8, 4, 2 or 1).
@@ -147,19 +174,18 @@ __device__ __forceinline__ mlpw_row<(N >= 64 ? N / 64 : 1)> mlpw_ld(const __attr
   return r;
 }
 
-// One layer over the listed inputs: y[c] = act(fmaf chain over the listed k,
+// One layer over the non-zero inputs: y[c] = act(fmaf chain over the set k,
 // ascending, of x[k] * W[k][c], from 0, + b[c]) for this lane's columns; the
-// rows (and their x[k]) run PF list entries ahead in a register ring.
+// rows (and their x[k]) run PF set bits ahead in a register ring.
 template <int K, int N, int PF, bool RELU>
 __device__ __forceinline__ void mlpw_layer(const float* Wl, const float* bias, const mlpw_lds_t* x,
-                                           const mlpw_lds_i16* list, int nnz, mlpw_lds_t* y) {
+                                           const MlpwMask& M, mlpw_lds_t* y) {
   constexpr int S = N >= 64 ? N / 64 : 1;
   const int lane = __lane_id();
   const __attribute__((address_space(1))) char* wb = (const __attribute__((address_space(1))) char*)mlpw_glb(Wl);
   const uint32_t voff = (uint32_t)(N >= 64 ? lane * S : (lane < N ? lane : N - 1)) * 4u;
-  auto kat = [&](int t) -> int {           // list entry t (clamped; row 0 when the list is empty)
-    return nnz ? __builtin_amdgcn_readfirstlane((int)list[t < nnz ? t : nnz - 1]) : 0;
-  };
+  const int nnz = M.nnz;
+  MlpwCursor cur{0, mlpw_chunk(M, 0)};
   float acc[S];
 #pragma unroll
   for (int s = 0; s < S; s++) acc[s] = 0.0f;
@@ -167,36 +193,41 @@ __device__ __forceinline__ void mlpw_layer(const float* Wl, const float* bias, c
   float xr[PF];
 #pragma unroll
   for (int i = 0; i < PF; i++) {
-    const int k = kat(i);
+    const int k = mlpw_next<K>(M, cur);
     w[i] = mlpw_ld<N>(wb, k, voff);
     xr[i] = x[k];
-    __builtin_amdgcn_sched_barrier(0);     // issue the ring in list order (the oldest rows are consumed first)
+    __builtin_amdgcn_sched_barrier(0);     // issue the ring in input order (the oldest rows are consumed first)
   }
-#pragma nounroll
-  for (int t0 = 0; t0 < nnz; t0 += PF) {
+  auto step = [&](int i) {
+    const float xv = xr[i];
+    if constexpr (S == 1) {
+      acc[0] = __builtin_fmaf(xv, w[i].v[0], acc[0]);
+    } else {
+      const mlpw_f2 xx = mlpw_f2{xv, xv};
 #pragma unroll
-    for (int i = 0; i < PF; i++) {
-      if (t0 + i < nnz) {
-        const float xv = xr[i];
-        if constexpr (S == 1) {
-          acc[0] = __builtin_fmaf(xv, w[i].v[0], acc[0]);
-        } else {
-          const mlpw_f2 xx = mlpw_f2{xv, xv};
-#pragma unroll
-          for (int s = 0; s < S; s += 2) {
-            const mlpw_f2 r = __builtin_elementwise_fma(xx, mlpw_f2{w[i].v[s], w[i].v[s + 1]},
-                                                        mlpw_f2{acc[s], acc[s + 1]});
-            acc[s] = r.x;
-            acc[s + 1] = r.y;
-          }
-        }
-        const int k = kat(t0 + i + PF);   // refill the slot PF entries ahead
-        w[i] = mlpw_ld<N>(wb, k, voff);
-        xr[i] = x[k];
-        __builtin_amdgcn_sched_barrier(0);
+      for (int s = 0; s < S; s += 2) {
+        const mlpw_f2 r = __builtin_elementwise_fma(xx, mlpw_f2{w[i].v[s], w[i].v[s + 1]},
+                                                    mlpw_f2{acc[s], acc[s + 1]});
+        acc[s] = r.x;
+        acc[s + 1] = r.y;
       }
     }
+    const int k = mlpw_next<K>(M, cur);     // refill the slot PF inputs ahead
+    w[i] = mlpw_ld<N>(wb, k, voff);
+    xr[i] = x[k];
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // whole rings without per-step guards (a guard would make the load-count
+  // waits conservative: every step would wait for nearly all loads in flight)
+  const int full = nnz - nnz % PF;
+#pragma nounroll
+  for (int t0 = 0; t0 < full; t0 += PF) {
+#pragma unroll
+    for (int i = 0; i < PF; i++) step(i);
   }
+#pragma unroll
+  for (int i = 0; i < PF - 1; i++)
+    if (i < nnz - full) step(i);
   mlpw_gf_t* bp = mlpw_glb(bias);
 #pragma unroll
   for (int s = 0; s < S; s++) {
@@ -215,24 +246,18 @@ __device__ __forceinline__ void mlpw_layer(const float* Wl, const float* bias, c
 // LDS writes before other lanes read them.
 __device__ __forceinline__ void mlpw_forward(const float* Q, mlpw_lds_t* R) {
   const bool skip = *(const __attribute__((address_space(1))) uint32_t*)(mlpw_glb(Q) + MLPW_FLAG) != 0u;
-  mlpw_lds_i16* l1 = (mlpw_lds_i16*)(R + MLPW_R_L1);
-  mlpw_lds_i16* ln = (mlpw_lds_i16*)(R + MLPW_R_LN);
   __syncthreads();
-  int n = mlpw_list<MLPW_IN>(R + MLPW_R_X, l1, skip);
+  MlpwMask M = mlpw_mask<MLPW_IN>(R + MLPW_R_X, skip);
+  mlpw_layer<MLPW_IN, MLPW_H1, 8, true>(Q + MLPW_L1, Q + MLPW_B1, R + MLPW_R_X, M, R + MLPW_R_H1);
   __syncthreads();
-  mlpw_layer<MLPW_IN, MLPW_H1, 8, true>(Q + MLPW_L1, Q + MLPW_B1, R + MLPW_R_X, l1, n, R + MLPW_R_H1);
+  M = mlpw_mask<MLPW_H1>(R + MLPW_R_H1, skip);
+  mlpw_layer<MLPW_H1, MLPW_H2, 12, true>(Q + MLPW_L2, Q + MLPW_B2, R + MLPW_R_H1, M, R + MLPW_R_H2);
   __syncthreads();
-  n = mlpw_list<MLPW_H1>(R + MLPW_R_H1, ln, skip);
+  M = mlpw_mask<MLPW_H2>(R + MLPW_R_H2, skip);
+  mlpw_layer<MLPW_H2, MLPW_H3, 16, true>(Q + MLPW_L3, Q + MLPW_B3, R + MLPW_R_H2, M, R + MLPW_R_H3);
   __syncthreads();
-  mlpw_layer<MLPW_H1, MLPW_H2, 12, true>(Q + MLPW_L2, Q + MLPW_B2, R + MLPW_R_H1, ln, n, R + MLPW_R_H2);
-  __syncthreads();
-  n = mlpw_list<MLPW_H2>(R + MLPW_R_H2, ln, skip);
-  __syncthreads();
-  mlpw_layer<MLPW_H2, MLPW_H3, 16, true>(Q + MLPW_L3, Q + MLPW_B3, R + MLPW_R_H2, ln, n, R + MLPW_R_H3);
-  __syncthreads();
-  n = mlpw_list<MLPW_H3>(R + MLPW_R_H3, ln, skip);
-  __syncthreads();
-  mlpw_layer<MLPW_H3, MLPW_OUT, 16, false>(Q + MLPW_L4, Q + MLPW_B4, R + MLPW_R_H3, ln, n, R + MLPW_R_LOGITS);
+  M = mlpw_mask<MLPW_H3>(R + MLPW_R_H3, skip);
+  mlpw_layer<MLPW_H3, MLPW_OUT, 16, false>(Q + MLPW_L4, Q + MLPW_B4, R + MLPW_R_H3, M, R + MLPW_R_LOGITS);
   __syncthreads();
   float sq[MLPW_OUT], s = 0.0f;
 #pragma unroll

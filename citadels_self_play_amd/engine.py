@@ -93,6 +93,13 @@ PRED_AHEAD = int(os.environ.get("CIT_PRED_AHEAD", "4"))
 PRED_FUSED = os.environ.get("CIT_PRED_FUSED", "1") != "0"
 PRED_SLICE_TICKS = int(os.environ.get("CIT_PRED_SLICE_TICKS", "0"))   # 1 / 2 / 3 / 4: 87.0k / 96.9k / 100.3k / 61.4k decisions/s (config 4, profiles/r03/pred_groups)
 _side_streams = {}
+# search-kernel launches made by this process, per kernel (bench.py's counter
+# child attributes each leg's dispatches with them)
+LAUNCHES = {}
+
+
+def _launched(kernel):
+    LAUNCHES[kernel] = LAUNCHES.get(kernel, 0) + 1
 
 
 def side_streams(device, n):
@@ -313,6 +320,7 @@ class GameBatch:
         o = self._orig(orig)
         chosen = torch.zeros((self.B, 16), dtype=torch.uint8, device=self.device)
         stats = torch.zeros((self.B, 5), dtype=torch.int32, device=self.device)
+        _launched("k_cfr_decide")
         _lib.check(self.lib.cit_cfr_decide(_ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt),
                                            _ptr(self.np_idx), _ptr(self.seer), self.B, int(iters), int(flags),
                                            None if o is None else _ptr(o), _ptr(self.pool),
@@ -477,6 +485,7 @@ class GameBatch:
         int32 CfrState, zero rows start a tree); `running` [1] int32 receives the
         count of trees left unfinished."""
         self._model_tree = False
+        _launched("k_cfr_train_slice")
         _lib.check(self.lib.cit_cfr_train_slice(
             _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx), _ptr(self.seer),
             self.B, int(iters), int(flags), None, _ptr(self.pool), self.node_cap, self.edge_cap, _ptr(self.optbuf),
@@ -561,6 +570,7 @@ class GameBatch:
         P = self._pred
         o = P["o"]
         stats = torch.empty((self.B, 5), dtype=torch.int32, device=self.device)
+        _launched("k_cfr_pred_fused")
         _lib.check(self.lib.cit_cfr_pred_fused(
             _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
             _ptr(self.seer), self.B, int(iters), int(flags), None if o is None else _ptr(o), int(max_depth),
@@ -575,6 +585,7 @@ class GameBatch:
         P = self._pred
         o = P["o"]
         w = _ptr(P["waiting"]) + 8 * slot
+        _launched("k_cfr_pred_step")
         _lib.check(self.lib.cit_cfr_pred_slice(
             _ptr(self.games), _ptr(self.mt), _ptr(self.mt_idx), _ptr(self.np_mt), _ptr(self.np_idx),
             _ptr(self.seer), self.B, int(iters), int(flags), None if o is None else _ptr(o), int(max_depth),

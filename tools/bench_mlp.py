@@ -18,9 +18,42 @@ FLOP_PER_ROW = 757_248
 PEAK_TF = 157.3
 
 
+def wave_latency(net):
+    """The single-row forward of the search's leaf evaluation
+    (cit_mlp_forward_wave, one row per wavefront): microseconds per launch of
+    M rows (M <= 1,024 rows run side by side, so the launch time is one
+    wavefront's latency), on encode_game-like sparse rows and on dense rows."""
+    for kind in ("sparse", "dense"):
+        for M in (1, 64, 512):
+            g = torch.Generator().manual_seed(M)
+            if kind == "sparse":      # ~80 of 418 features set, small counts (an encode_game row's shape)
+                x = (torch.rand((M, 418), generator=g) < 0.2).float() * torch.randint(1, 4, (M, 418), generator=g)
+            else:
+                x = torch.rand((M, 418), generator=g) + 0.1
+            x = x.cuda()
+            probs = torch.empty((M, 6), device="cuda")
+            call = lambda: net.lib.cit_mlp_forward_wave(x.data_ptr(), M, net.wave.data_ptr(), probs.data_ptr(), None,
+                                                       torch.cuda.current_stream().cuda_stream)
+            for _ in range(3):
+                call()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n = 50
+            e0.record()
+            for _ in range(n):
+                call()
+            e1.record()
+            torch.cuda.synchronize()
+            print(json.dumps({"schedule": "wave", "rows": M, "input": kind, "nnz_mean": float((x != 0).sum(1).float().mean()),
+                              "us_per_call": e0.elapsed_time(e1) * 1e3 / n}), flush=True)
+
+
 def main():
     torch.manual_seed(0)
     net = models.ValueNet(models.ValueOnlyNN(418, 512).eval(), "cuda")
+    wave_latency(net)
+    if "--wave-only" in sys.argv:
+        return
     for fused in (False, True):
         for M in (512, 1024, 1365, 2048, 4096, 8192):
             x = torch.randint(0, 4, (M, 418), device="cuda").float()

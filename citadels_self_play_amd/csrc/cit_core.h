@@ -89,8 +89,9 @@ __device__ __forceinline__ uint64_t cit_wave_or64(uint64_t v) {
 #define CIT_ERR_STEP_CAP 0x100u    // rollout hit its hard step cap (the reference has no cap)
 // With CIT_ERR_OVERFLOW, which MCCFR node-pool capacity ran out (a search run
 // again with more room gives the reference's tree; an overflow without these
-// bits is an engine list capacity, e.g. a museum of more than 16 cards, that
-// no retry fixes):
+// bits is an engine list capacity that no retry fixes: a player holding more
+// than CIT_AREA_CAP cards in hand + just-drawn + museum, or more than
+// CIT_KH_MAX HandKnowledge entries):
 #define CIT_ERR_POOL_ARENA 0x1000u // the shared block arena was exhausted
 #define CIT_ERR_POOL_CAP 0x2000u   // the tree reached its node / edge caps
 #define CIT_ERR_POOL_ROW 0x4000u   // a node row differs from the base row in more dwords than a diff slot holds

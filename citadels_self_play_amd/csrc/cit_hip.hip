@@ -14,7 +14,9 @@
 // shuffle_seq): the rollout's one batch 0.92 -> 0.94 G, the overlapped
 // headline unchanged (profiles/r04/rollout_waves/summary_shuffle.txt); the
 // search unit keeps the LDS swaps (8 % slower there: its registers are full)
+#ifndef CIT_SHUFFLE_REG
 #define CIT_SHUFFLE_REG 1
+#endif
 
 #include "../../include/citadels.h"
 #include "cit_area_test.h"

@@ -111,6 +111,8 @@ ARENA_MIN_TREES, ARENA_MIN_BLOCKS = 32, 16
 # 1.25 61.4, 1.5 65.4 / 77.4, 2.0 61.0 (round 2's best), 2.5 63.2, 3.0 60.9
 # trees/s.
 QUEUE_OVERCOMMIT = float(os.environ.get("CIT_QUEUE_OVERCOMMIT", "1.5"))
+# wall-clock seconds per queue slice (cit_cfr_train_slice's budget)
+QUEUE_SLICE_S = float(os.environ.get("CIT_QUEUE_SLICE_S", "0.5"))
 
 
 def arena_frac_for(B, node_cap):
@@ -254,7 +256,7 @@ class _SlicePlanner:
 
 
 def simulate_queue(seeds, iters, slots=None, max_move=100, node_cap=None, edge_cap=None, device=None,
-                   slice_seconds=0.5, max_pool_bytes=None, arena_frac="auto", log=None, overcommit=None,
+                   slice_seconds=None, max_pool_bytes=None, arena_frac="auto", log=None, overcommit=None,
                    max_requeue=0):
     """simulate_games through a tree queue: `slots` trees search at once (one
     per workgroup, sharing one block arena); the search runs in slices of
@@ -321,7 +323,7 @@ class TreeQueue:
     sizes them for a batch of that many positions."""
 
     def __init__(self, iters, per_round, slots=None, max_move=100, node_cap=None, edge_cap=None, device=None,
-                 slice_seconds=0.5, max_pool_bytes=None, arena_frac="auto", log=None, overcommit=None,
+                 slice_seconds=None, max_pool_bytes=None, arena_frac="auto", log=None, overcommit=None,
                  max_requeue=0, multi_round=True):
         from .engine import pool_bytes, side_streams, row_cap_for
         from . import layout as L
@@ -370,7 +372,7 @@ class TreeQueue:
         self.pending = None                   # (slots, global ids) finished last slice: targets walked during this one
         self.requeue, self.retries = [], {}
         self.n_slices = self.n_requeued = 0
-        self.ticks = max(1, int(slice_seconds * 1e8))
+        self.ticks = max(1, int((QUEUE_SLICE_S if slice_seconds is None else slice_seconds) * 1e8))
         self.ran = np.zeros(S, bool)
         self.side, self.rstream = side_streams(dev, 2)
         self.planner = None

@@ -240,8 +240,9 @@ int cit_cfr_opt_cap(void);             /* CitOption scratch per tree (optbuf) */
  * with CIT_ERR_OVERFLOW (0x1), which node-pool capacity ran out -- 0x1000 the
  * shared arena, 0x2000 the tree's node / edge caps (rows included), 0x4000 a diff row past row_cap.
  * Only these are worth a second search (with more room / raw rows); an
- * overflow without them is an engine list capacity (e.g. a museum of more
- * than 16 cards) that no retry fixes. */
+ * overflow without them is an engine list capacity (a player holding more
+ * than 88 cards in hand + just-drawn + museum, or more than 32 HandKnowledge
+ * entries) that no retry fixes. */
 
 /* The config-3 position harness: k = random.randint(lo, hi) drawn from the
  * lane's stream, then k random-policy steps (stops at a winner). */

@@ -514,7 +514,10 @@ class TreeQueue:
                     t = sb._cfr_targets(roots, 0)
                     for R, loc, sl in self._split(p_qs, p_slots):
                         R.parts.append((t, sl, loc))
-            torch.cuda.synchronize()
+            # the slice and the walk -- not the device: an overflowed tree searched again on the
+            # retry stream (seconds for a 200k tree) must not hold the queue's next slice
+            torch.cuda.current_stream(dev).synchronize()
+            self.side.synchronize()
             tq = self._tick("slice+targets", tq)
             if paused is not None:
                 state[paused, 6] = saved

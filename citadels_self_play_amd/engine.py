@@ -138,6 +138,15 @@ def pool_bytes(B, node_cap, edge_cap, frac=None, row_cap="auto", pred=False):
     return B * L.cfr_pool_bytes(node_cap, edge_cap) + L.cfr_arena_bytes(nb, eb, rc, pred)
 
 
+def device_avail_bytes(device):
+    """Device bytes a new pool may take: free memory plus what torch's caching
+    allocator holds but does not use (a released node pool stays cached, so
+    the next search of the same size reuses it instead of a fresh hipMalloc of
+    up to ~230 GB; torch frees cached blocks itself if a request does not fit)."""
+    free = torch.cuda.mem_get_info(device)[0]
+    return free + torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+
+
 def _ptr(t):
     return t.data_ptr()
 
@@ -458,7 +467,7 @@ class GameBatch:
         need = per * self.B + self.lib.cit_cfr_arena_bytes_fmt(nb, eb, rc, int(pred))
         have = self.pool.numel() if getattr(self, "pool", None) is not None else 0
         if need > have and self.device.type == "cuda":
-            avail = int(0.9 * (torch.cuda.mem_get_info(self.device)[0] + have))
+            avail = int(0.9 * (device_avail_bytes(self.device) + have))
             if need > avail:
                 nbt, ebt = L.cfr_nblocks(node_cap), L.cfr_eblocks(edge_cap)
                 scale = max(0.0, (avail - per * self.B) / float(need - per * self.B))

@@ -149,8 +149,8 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
     edge_cap = edge_cap or 5 * node_cap
     dev = torch.device(device or "cuda")
     if max_pool_bytes is None:
-        torch.cuda.empty_cache()                # cached blocks of earlier pools count as free
-        max_pool_bytes = int(0.8 * torch.cuda.mem_get_info(dev)[0])
+        from .engine import device_avail_bytes   # (cached blocks of earlier pools count as free)
+        max_pool_bytes = int(0.8 * device_avail_bytes(dev))
     seeds = np.asarray(seeds, np.int64)
     frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
     chunk = len(seeds)
@@ -336,8 +336,8 @@ class TreeQueue:
         dev = self.dev = torch.device(device or "cuda")
         self.t_setup = time.perf_counter()
         if max_pool_bytes is None:
-            torch.cuda.empty_cache()
-            max_pool_bytes = int(0.8 * torch.cuda.mem_get_info(dev)[0])
+            from .engine import device_avail_bytes
+            max_pool_bytes = int(0.8 * device_avail_bytes(dev))
         frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
         Q = max(1, int(per_round))
         S = min(Q, slots or Q)

@@ -53,15 +53,19 @@ def node_arrays(nodes, edges, n):
 
 
 def pool_caps(iters):
-    """Node / edge capacity for a cfr_train(iters) tree: measured 1.2-3.3 nodes
-    per iteration (2000 iterations: up to 6,604 nodes; 200000: up to 646,897)
-    and up to ~4 edge slots per node (~2 measured since opponent nodes' runs
-    grow as they fill), plus ROW_EDGE_SLOTS per node for the diff rows of
-    large trees (row_cap_for: ~7 slots measured); a tree that
-    still outgrows its pool is searched again with a 4x pool
-    (GameBatch._retry_overflow).  Caps bound a tree; the arena holds what the
-    trees use."""
-    node_cap = max(1024, int(3.5 * iters) + 512)
+    """Node / edge capacity for a cfr_train(iters) tree: measured 1.2-3.5 nodes
+    per iteration (2000 iterations: up to 6,604 nodes; 200000: up to 646,897
+    in 10,000 trees, and one past 700,512 in the next 3,840) and up to ~4
+    edge slots per node (~2 measured since opponent nodes' runs grow as they
+    fill), plus ROW_EDGE_SLOTS per node for the diff rows of large trees
+    (row_cap_for: ~7 slots measured); caps are 1.3x the 3.5 nodes per
+    iteration that bounded round 4's trees, because a tree that still
+    outgrows its pool is searched again from the start with a 4x pool
+    (GameBatch._retry_overflow) -- alone at the end of a data round that is
+    ~13 s of one wavefront.  Caps bound a tree's tables (224 node / 778 edge
+    blocks at 200k, under CFR_TBL_MAX); the arena holds what the trees use
+    (selfplay.ARENA_FRAC is relative to these caps)."""
+    node_cap = max(1024, int(4.55 * iters) + 512)
     rows = ROW_EDGE_SLOTS * node_cap if row_cap_for(node_cap) else 0
     return node_cap, 4 * node_cap + 4096 + rows
 

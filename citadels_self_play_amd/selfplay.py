@@ -99,11 +99,11 @@ def decide(seeds, iters, net=None, lo=0, hi=300, node_cap=None, device=None, fus
 
 # Arena share of the trees' worst case (node blocks, edge blocks) for batches of
 # >= ARENA_MIN_TREES trees of >= ARENA_MIN_BLOCKS node blocks each: cfr_train(200000)
-# trees average ~1.35 nodes / iteration against pool_caps' 3.5,
+# trees average ~1.35 nodes / iteration against round 4's caps of 3.5,
 # and ~9 edge slots per node (children ~2, row ~7) against its 4 +
-# ROW_EDGE_SLOTS: about 0.38 and 0.25 of the caps, so node and edge blocks run
-# out together.
-ARENA_FRAC = (0.5, 0.33)
+# ROW_EDGE_SLOTS: about 0.38 and 0.25 of those caps, so node and edge blocks run
+# out together; pool_caps is now 1.3x those caps, the fractions 1/1.3 of round 4's.
+ARENA_FRAC = (0.385, 0.254)      # round 4's (0.5, 0.33) of the 1.3x smaller caps (engine.pool_caps)
 ARENA_MIN_TREES, ARENA_MIN_BLOCKS = 32, 16
 # Tree-queue slots per slot that fits at ARENA_FRAC (simulate_queue's overcommit).
 # With diff row slots a slot is smaller, so fewer paused trees pay: 1920 trees

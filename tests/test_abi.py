@@ -81,8 +81,10 @@ def test_arena_blocks():
     assert pool_bytes(2, 700_512, 2_806_144) == 2 * L.cfr_pool_bytes(700_512, 2_806_144) + \
         L.cfr_arena_bytes(344, 344, 388, False)                # large trees: diff rows, no pred
     from citadels_self_play_amd.engine import pool_caps
-    assert pool_caps(200000) == (700_512, 14 * 700_512 + 4096)   # row runs in the edge cap
-    assert pool_caps(200) == (1212, 4 * 1212 + 4096)            # small trees: raw rows
+    assert pool_caps(200000) == (910_512, 14 * 910_512 + 4096)   # row runs in the edge cap
+    assert pool_caps(200) == (1422, 4 * 1422 + 4096)            # small trees: raw rows
+    nc, ec = pool_caps(200000)
+    assert L.cfr_nblocks(nc) <= 1024 and L.cfr_eblocks(ec) <= 1024  # the tables fit a tree's LDS copy
 
 
 def test_bad_args_rejected(lib):

@@ -55,10 +55,13 @@ Prints ONE JSON line on rank 0.  `value` = carry_out transitions of all ranks
   `hbm_notional` keeps SURVEY §8(d)'s bytes per child created:
     3: 1024 positions per GPU, one cfr_train(200) decision each (no NN)
     4: 4096 positions over the job (4096 / N per GPU), cfr_pred(200, depth 10)
-       with ValueOnlyNN(418, 512) weights from torch.manual_seed(0)
+       with ValueOnlyNN(418, 512) weights from torch.manual_seed(0), one
+       launch (k_cfr_pred_fused: each tree evaluates its leaves in its kernel)
     5: --cfg5-trees simulate_game trees per GPU at cfr_train(--cfg5-iters)
        (default 200000, the reference's own setting) through the tree queue,
-       targets pooled with the RCCL all-gather
+       targets pooled with the RCCL all-gather; `value` = --cfg5-rounds data
+       rounds through one cross-round queue (train_from_scratch's loop),
+       `value_one_batch` = one round alone
   `4@512` and `5@960` run configs 4 and 5 at the per-rank shard of the 8-GPU
   job (4096 / 8 positions; train_from_scratch's --games-per-gpu trees).
   Config 3's `value` runs consecutive batches on --cfr-streams HIP streams
@@ -789,7 +792,10 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
         5: "config5: %d simulate_game trees per GPU: create_a_random_game(100) -> cfr_train(%d) -> "
            "get_all_targets(200), tree queue, targets all-gathered" % (per_gpu, iters)}[config],
         "per_gpu": per_gpu,
-        "value": streams["value"] if streams else med["value"], "unit": "trees/s" if config == 5 else "decisions/s",
+        # a continuous loop where the workload is one (config 3: consecutive batches on streams; config 5:
+        # data rounds through one tree queue), value_one_batch the median of one batch / round alone
+        "value": streams["value"] if streams else rounds["value"] if rounds else med["value"],
+        "unit": "trees/s" if config == 5 else "decisions/s",
         "value_one_batch": med["value"], "streams": streams, "rounds": rounds,
         "carry_out_per_s": med["carry_out_per_s"], "reps": len(reps), "median": med,
         "all_reps_value": [r["value"] for r in reps],
@@ -883,12 +889,14 @@ def _cfg5_rounds(args, world, rank, dev, iters, per_gpu):
                                             maxes=tuple(range(0, 1)) + tuple(range(4, 4 + R)))
     gaps = np.diff(done)
     return {"value": trees / el, "unit": "trees/s", "rounds": R, "trees_per_round": per_gpu * world,
-            "seconds": el, "round_done_s": done, "steady_state": per_gpu * world / float(np.mean(gaps)),
+            "seconds": el, "round_done_s": done,
+            "after_first_round": per_gpu * world * (R - 1) / float(done[-1] - done[0]) if R > 1 else None,
             "first_round_s": done[0], "carry_out_per_s": carry / el, "error_lanes": int(errs),
             "pooled_targets": n_targets, "slots": S, "overcommit": oc,
             "note": "rounds of trees through one TreeQueue, all added up front (the next round's trees take the "
-                    "slots the current round's tail frees); steady_state = trees per round / mean gap between "
-                    "round completions"}
+                    "slots the current round's tail frees); value = all trees / the whole run (first round's ramp "
+                    "and last round's tail included); after_first_round = the later rounds' trees / the time "
+                    "between the first and the last round's completion (they started earlier: an upper figure)"}
 
 
 def _cpu_model():

@@ -993,6 +993,11 @@ def main():
                    "roofline": c["roofline"], "cpu_baseline": c.get("cpu_baseline"), "cfr": c}
     cfr_out = {}
     for key in cfr_list:
+        # each leg starts from an empty allocator cache (outside every timed region): the legs' node
+        # pools differ in size, and one leg's cached arena must not crowd the next leg's
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
         try:
             c, _, n = key.partition("@")
             c = int(c)

@@ -643,6 +643,8 @@ class TreeQueue:
         return R.src, R.out_stats, t
 
     def close(self):
+        """Release the pool (the planner's view of the block tables included)
+        and the rounds' target parts (their results were assembled)."""
         if self.qtrace is not None:
             self.qtrace.close()
             self.qtrace = None
@@ -650,6 +652,9 @@ class TreeQueue:
             torch.cuda.synchronize()
             self.sb.pool = None
             self.sb = None
+        self.planner = None
+        for R in self.rounds:
+            R.parts, R.early, R.snap = [], [], None
 
 
 def _pad_lanes(b, S):

@@ -387,7 +387,11 @@ class TreeQueue:
     def add(self, seeds):
         """Append a round of positions (random.seed(s), np.random.seed(s),
         create_a_random_game(max_move) per seed); returns its index."""
+        t_pos = time.perf_counter()
         r = _Round(seeds, self.total, self.max_move, self.dev)
+        if self.log is not None:
+            torch.cuda.synchronize()
+            t_pos = time.perf_counter() - t_pos
         self.total += r.Q
         self.rounds.append(r)
         if self.sb is None:
@@ -404,8 +408,8 @@ class TreeQueue:
                 self.overcommit > 1 or (self.arena_f is not None and self.multi_round)) else None
             if self.log is not None:
                 torch.cuda.synchronize()
-                self.log("simulate_queue: %d positions and a %d-slot pool set up in %.1f s"
-                         % (r.Q, self.S, time.perf_counter() - self.t_setup))
+                self.log("simulate_queue: %d positions and a %d-slot pool set up in %.1f s (positions %.2f s)"
+                         % (r.Q, self.S, time.perf_counter() - self.t_setup, t_pos))
         self._admit()
         return len(self.rounds) - 1
 

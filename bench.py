@@ -930,8 +930,9 @@ def main():
     ap.add_argument("--cfr-reps", type=int, default=5, help="timed reps of configs 3 and 4 (median reported)")
     ap.add_argument("--cfg5-reps", type=int, default=1, help="timed reps of config 5")
     ap.add_argument("--cfr-cpu-seconds", type=float, default=4.0, help="per C++ CPU-baseline leg of configs 3-5")
-    ap.add_argument("--cfr-streams", type=int, default=2, help="config 3: HIP streams for consecutive batches")
-    ap.add_argument("--cfr-stream-batches", type=int, default=8, help="config 3: batches in the streams run")
+    ap.add_argument("--cfr-streams", type=int, default=3,
+                    help="config 3: HIP streams for consecutive batches (3: 169-172 k vs 2: 124 k vs 4: 120-122 k, 'profiles/r05/config3_streams')")
+    ap.add_argument("--cfr-stream-batches", type=int, default=12, help="config 3: batches in the streams run")
     ap.add_argument("--cfg5-trees", type=int, default=1920, help="config 5 trees per GPU")
     ap.add_argument("--cfg5-iters", type=int, default=200000, help="config 5 cfr_train iterations per tree")
     ap.add_argument("--cfg5-rounds", type=int, default=3,

@@ -979,6 +979,73 @@ struct BufSink {
   CIT_WAVE_LIST_EMIT
 };
 
+#if CIT_WAVE
+// BufSink's list held in registers instead of LDS: lane i keeps option i (the
+// first 64; more are only counted), so a serial emit is four lane selects
+// and the draw four readlanes -- no LDS store per option, no LDS round trip
+// for the pick.  A lane-parallel emit moves the proposals to lanes n + rank
+// with one ds_permute per word (a bijection: the other lanes go to the
+// remaining lanes, which keep their words).
+struct RegSink {
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  int n = 0;
+  uint32_t err = 0;
+  __device__ __forceinline__ void put(const CitOpt& o) {
+    uint32_t w[4];
+    __builtin_memcpy(w, &o, 16);
+    const bool me = (int)__lane_id() == n;
+    r0 = me ? w[0] : r0;
+    r1 = me ? w[1] : r1;
+    r2 = me ? w[2] : r2;
+    r3 = me ? w[3] : r3;
+  }
+  __device__ bool emit(const CitOpt& o) {
+    if (n < 64) put(o);
+    n++;
+    return false;
+  }
+  template <class F> __device__ bool block(int cnt, F&& f) {
+    int m = 64 - n < cnt ? 64 - n : cnt;
+    for (int i = 0; i < m; i++) {
+      put(f(i));
+      n++;
+    }
+    n += cnt - (m > 0 ? m : 0);
+    return false;
+  }
+  __device__ bool wave_emit(bool p, const CitOpt& o) {
+    const uint64_t m = cit_ballot(p);
+    const int c = __popcll(m);
+    if (c && n < 64) {
+      const int ln = (int)__lane_id();
+      const int dst = (n + (p ? cit_lane_rank(m) : c + cit_lane_rank(~m))) & 63;
+      uint32_t w[4];
+      __builtin_memcpy(w, &o, 16);
+      const int a = dst << 2;
+      const uint32_t q0 = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)w[0]);
+      const uint32_t q1 = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)w[1]);
+      const uint32_t q2 = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)w[2]);
+      const uint32_t q3 = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)w[3]);
+      const bool mine = ln >= n && ln < n + c;
+      r0 = mine ? q0 : r0;
+      r1 = mine ? q1 : r1;
+      r2 = mine ? q2 : r2;
+      r3 = mine ? q3 : r3;
+    }
+    n += c;
+    return false;
+  }
+  // option k < 64 (k wave-uniform)
+  __device__ __forceinline__ CitOpt at(int k) const {
+    uint32_t w[4] = {(uint32_t)__builtin_amdgcn_readlane((int)r0, k), (uint32_t)__builtin_amdgcn_readlane((int)r1, k),
+                     (uint32_t)__builtin_amdgcn_readlane((int)r2, k), (uint32_t)__builtin_amdgcn_readlane((int)r3, k)};
+    CitOpt o;
+    __builtin_memcpy(&o, w, 16);
+    return o;
+  }
+};
+#endif
+
 // skip_false_choice only asks whether a state has exactly one option: this
 // sink lists like ListSink but, when `stop` is set, ends the enumeration once
 // a second option is known (n is then a lower bound >= 2).  Callers clear
@@ -2682,6 +2749,24 @@ CIT_HD int cit_random_step_buf(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* b
   int w = cit_carry_out(g, o, rng);
   return (w >= 0 || g.err || g.terminal) ? 1 : 0;
 }
+
+#if CIT_WAVE
+// cit_random_step_buf with the list in registers (RegSink, at most 64 listed)
+__device__ __forceinline__ int cit_random_step_reg(CitGame& g, CitMT& rng, uint64_t* seer) {
+  cit_prepare_options(g, rng, seer);
+  RegSink s;
+  cit_enum_options(g, s, seer);
+  if (s.err) { g.err |= s.err; return 1; }
+  int n = s.n;
+  if (n == 0) { g.err |= CIT_ERR_EMPTY; return 1; }
+  int k = (int)mt_randbelow(rng, (uint32_t)n);
+  CitOpt o = k < 64 ? s.at(k) : cit_pick_option(g, k, seer);
+  int w = cit_carry_out(g, o, rng);
+  return (w >= 0 || g.err || g.terminal) ? 1 : 0;
+}
+#elif defined(__HIPCC__)
+__device__ int cit_random_step_reg(CitGame& g, CitMT& rng, uint64_t* seer);   // (host pass: kernels only)
+#endif
 
 // One random-policy step (compare_to_random.py:37-39): get_options ->
 // random.choice -> carry_out.  Returns 1 when the lane is done (winner or error).

@@ -29,6 +29,9 @@ static_assert(sizeof(CitOpt) == sizeof(CitOption), "descriptor layouts differ");
 #ifndef ROLLOUT_BUF
 #define ROLLOUT_BUF 64   // options listed per step; 64 measured 1.3-1.5 % over 32 (preset max 56)
 #endif
+#ifndef ROLLOUT_REG
+#define ROLLOUT_REG 1   // the step's option list in registers (RegSink) instead of buf
+#endif
 
 namespace {
 
@@ -345,7 +348,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROLL_WAVES_P
       for (int i = 0; i < 160; i++) atomicAdd(&g_roll_prof[i], acc[i]);
 #else
     while (!g.terminal && !g.err && s < cap) {
-      if (ROLLOUT_BUF) cit_random_step_buf(g, r, sc, buf, ROLLOUT_BUF);
+      if (ROLLOUT_REG) cit_random_step_reg(g, r, sc);
+      else if (ROLLOUT_BUF) cit_random_step_buf(g, r, sc, buf, ROLLOUT_BUF);
       else cit_random_step(g, r, sc);
       s++;
     }
@@ -382,7 +386,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROLL_WAVES_P
       int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
       int s = 0;
       while (!gm.terminal && !gm.err && s < cap) {
-        if (ROLLOUT_BUF) cit_random_step_buf(gm, r, sc, buf, ROLLOUT_BUF);
+        if (ROLLOUT_REG) cit_random_step_reg(gm, r, sc);
+        else if (ROLLOUT_BUF) cit_random_step_buf(gm, r, sc, buf, ROLLOUT_BUF);
         else cit_random_step(gm, r, sc);
         s++;
       }

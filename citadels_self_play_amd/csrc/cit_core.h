@@ -40,6 +40,14 @@ __device__ __forceinline__ uint64_t cit_ballot(bool p) { return (uint64_t)__ball
 __device__ __forceinline__ int cit_readlane(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
 __device__ __forceinline__ int cit_writelane(int v, int val, int i) { return (int)__lane_id() == i ? val : v; }
 __device__ __forceinline__ uint64_t cit_below() { return (1ull << __lane_id()) - 1; }   // lanes under this one
+// a[i] where ok, else z: every lane loads (a lane that is not ok reads a[0],
+// which every list the engine scans has), so no exec-mask branch is built
+// around the load -- `ok ? a[i] : z` is a divergent branch to the compiler.
+template <class T>
+__device__ __forceinline__ int cit_ld(const T* a, int i, bool ok, int z) {
+  const int v = (int)a[ok ? i : 0];
+  return ok ? v : z;
+}
 extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_or_u32(unsigned int);
 __device__ __forceinline__ uint64_t cit_wave_or64(uint64_t v) {
   return ((uint64_t)__ockl_wfred_or_u32((unsigned int)(v >> 32)) << 32) | __ockl_wfred_or_u32((unsigned int)v);
@@ -450,7 +458,8 @@ CIT_HD uint32_t mt_next(CitMT& r) {
     int b = (int)(i & ~63u);
     if (b != r.win_base) {
       int j = b + (int)__lane_id();
-      r.win = mt_temper(j < CIT_MT_N ? ((const cit_lds_u32*)r.mt)[j] : 0u);
+      const uint32_t wj = ((const cit_lds_u32*)r.mt)[j < CIT_MT_N ? j : 0];   // every lane loads (no branch)
+      r.win = mt_temper(j < CIT_MT_N ? wj : 0u);
       r.win_base = b;
     }
     return (uint32_t)__builtin_amdgcn_readlane((int)r.win, (int)(i & 63u));

@@ -17,7 +17,7 @@ CIT_HD bool has_type(const uint8_t* a, int n, int t) {
 #if CIT_WAVE
   if (n <= 64) {
     int i = cit_lane();
-    return cit_ballot(i < n && card_type(a[i]) == t) != 0;
+    return cit_ballot((i < n) & (card_type(cit_ld(a, i, i < n, 0)) == t)) != 0;
   }
 #endif
   for (int i = 0; i < n; i++)
@@ -28,7 +28,7 @@ CIT_HD int count_type(const uint8_t* a, int n, int t) {
 #if CIT_WAVE
   if (n <= 64) {
     int i = cit_lane();
-    return __popcll(cit_ballot(i < n && card_type(a[i]) == t));
+    return __popcll(cit_ballot((i < n) & (card_type(cit_ld(a, i, i < n, 0)) == t)));
   }
 #endif
   int k = 0;
@@ -39,7 +39,7 @@ CIT_HD int count_suit(const uint8_t* a, int n, int s) {
 #if CIT_WAVE
   if (n <= 64) {
     int i = cit_lane();
-    return __popcll(cit_ballot(i < n && card_suit(a[i]) == s));
+    return __popcll(cit_ballot((i < n) & (card_suit(cit_ld(a, i, i < n, 0)) == s)));
   }
 #endif
   int k = 0;
@@ -54,8 +54,8 @@ CIT_HD int take_like(uint8_t* a, uint8_t& n, int c) {
   int cnt = n;
   if (cnt <= 64) {
     int j = cit_lane();
-    int v = j < cnt ? a[j] : CIT_NO_CARD;
-    uint64_t m = cit_ballot(j < cnt && card_type(v) == t);
+    int v = cit_ld(a, j, j < cnt, CIT_NO_CARD);
+    uint64_t m = cit_ballot((j < cnt) & (card_type(v) == t));
     if (!m) return c;
     int i = __ffsll((unsigned long long)m) - 1;
     int r = cit_readlane(v, i);
@@ -95,7 +95,7 @@ CIT_HD int pop_front(uint8_t* a, uint8_t& n) {
   int cnt = n;
   if (cnt <= 64) {
     int j = cit_lane();
-    int v = j < cnt ? a[j] : 0;
+    int v = cit_ld(a, j, j < cnt, 0);
     int r = cit_readlane(v, 0);
     if (j >= 1 && j < cnt) a[j - 1] = (uint8_t)v;
     n = (uint8_t)(cnt - 1);
@@ -112,7 +112,7 @@ CIT_HD int pop_front(uint8_t* a, uint8_t& n) {
 struct ByteList {
 #if CIT_WAVE
   int v;
-  CIT_HD ByteList(const uint8_t* a, int n) { int i = cit_lane(); v = i < n ? a[i] : 0; }
+  CIT_HD ByteList(const uint8_t* a, int n) { int i = cit_lane(); v = cit_ld(a, i, i < n, 0); }
   CIT_HD int operator[](int i) const { return cit_readlane(v, i); }
 #else
   const uint8_t* a;
@@ -157,8 +157,10 @@ CIT_HD void area_splice(CitGame& g, CitPlayer& P, int L, int at, int del, int in
 #if CIT_WAVE
   {
     const int l = cit_lane(), j0 = cut + del + l, j1 = j0 + 64;
-    const int v0 = j0 < used ? P.hand[j0] : 0, v1 = j1 < used ? P.hand[j1] : 0;
-    const int s0 = l < ins ? (int)src(l) : 0, s1 = l + 64 < ins ? (int)src(l + 64) : 0;
+    // the first halves load on every lane (no branch); the second halves (past
+    // lane 64: rarely any lane) keep the branch that skips them
+    const int v0 = cit_ld(P.hand, j0, j0 < used, 0), v1 = j1 < used ? P.hand[j1] : 0;
+    const int s0 = (int)src(l), s1 = l + 64 < ins ? (int)src(l + 64) : 0;   // (src is safe past ins)
     __asm__ volatile("" ::: "memory");   // every byte loaded before any is stored
     if (j0 < used) P.hand[j0 - del + ins] = (uint8_t)v0;
     if (j1 < used) P.hand[j1 - del + ins] = (uint8_t)v1;
@@ -192,8 +194,8 @@ CIT_HD int pl_take_like(CitGame& g, CitPlayer& P, int L, int c) {
 #if CIT_WAVE
   {
     const int used = area_used(P), l = cit_lane(), p0 = off + l, p1 = p0 + 64;
-    const int v0 = p0 < used ? P.hand[p0] : 0, v1 = p1 < used ? P.hand[p1] : 0;
-    const uint64_t m0 = cit_ballot(l < n && card_type(v0) == t), m1 = cit_ballot(l + 64 < n && card_type(v1) == t);
+    const int v0 = cit_ld(P.hand, p0, p0 < used, 0), v1 = p1 < used ? P.hand[p1] : 0;
+    const uint64_t m0 = cit_ballot((l < n) & (card_type(v0) == t)), m1 = cit_ballot((l + 64 < n) & (card_type(v1) == t));
     if (!(m0 | m1)) return c;
     const int i = m0 ? __ffsll((unsigned long long)m0) - 1 : 64 + __ffsll((unsigned long long)m1) - 1;
     const int r = i < 64 ? cit_readlane(v0, i) : cit_readlane(v1, i - 64);
@@ -284,9 +286,9 @@ CIT_HD int deck_take_like(CitGame& g, int c) {
   {   // lanes l / 64 + l hold logical positions l / 64 + l; one ballot finds the
       // first match, every lane loads before any lane stores the shifted tail
     const int nd = g.n_deck, head = g.deck_head, l = cit_lane();
-    int c0 = l < nd ? g.deck[(head + l) & (CIT_DECK_CAP - 1)] : CIT_NO_CARD;
+    int c0 = cit_ld(g.deck, (head + l) & (CIT_DECK_CAP - 1), l < nd, CIT_NO_CARD);
     int c1 = l + 64 < nd ? g.deck[(head + l + 64) & (CIT_DECK_CAP - 1)] : CIT_NO_CARD;
-    uint64_t m0 = cit_ballot(l < nd && card_type(c0) == t), m1 = cit_ballot(l + 64 < nd && card_type(c1) == t);
+    uint64_t m0 = cit_ballot((l < nd) & (card_type(c0) == t)), m1 = cit_ballot((l + 64 < nd) & (card_type(c1) == t));
     if (!(m0 | m1)) return c;
     int i = m0 ? __ffsll((unsigned long long)m0) - 1 : 64 + __ffsll((unsigned long long)m1) - 1;
     int r = i < 64 ? cit_readlane(c0, i) : cit_readlane(c1, i - 64);
@@ -438,7 +440,7 @@ CIT_HD void kh_take_like(CitGame& g, int e, int c) {
       int cnt = fill - s0;
       int w[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) w[k] = l + 64 * k < cnt ? g.kh_pool[s0 + l + 64 * k] : 0;
+      for (int k = 0; k < 4; k++) w[k] = k ? (l + 64 * k < cnt ? g.kh_pool[s0 + l + 64 * k] : 0) : cit_ld(g.kh_pool, s0 + l, l < cnt, 0);
       __asm__ volatile("" ::: "memory");   // every byte loaded before any is moved
 #pragma unroll
       for (int k = 0; k < 4; k++)
@@ -529,7 +531,8 @@ CIT_HD int holder(const CitGame& g, int rid) {
 #if CIT_WAVE
   {
     int i = cit_lane();
-    uint64_t m = cit_ballot(i < CIT_NP && g.pl[i < CIT_NP ? i : 0].role == want);
+    const int ri = g.pl[i < CIT_NP ? i : 0].role;
+    uint64_t m = cit_ballot((i < CIT_NP) & (ri == want));
     return m ? __ffsll((unsigned long long)m) - 1 : -1;
   }
 #endif
@@ -634,7 +637,8 @@ CIT_HD void setup_next_player(CitGame& g, int current) {
 #if CIT_WAVE
     {
       int k = cit_lane(), nu = g.n_used_roles;
-      uint64_t m = cit_ballot(k < nu && k < CIT_NP && g.used_roles[k < CIT_NP ? k : 0] == r);
+      const int uk = g.used_roles[k < CIT_NP ? k : 0];
+      uint64_t m = cit_ballot((k < nu) & (k < CIT_NP) & (uk == r));
       if (nu <= CIT_NP) i = m ? __ffsll((unsigned long long)m) - 1 : -1;
       else
         for (int kk = 0; kk < nu; kk++)
@@ -671,10 +675,11 @@ CIT_HD void cit_setup_round(CitGame& g, CitMT& rng) {
 #if CIT_WAVE
   {
     int i = cit_lane();
-    uint64_t m = cit_ballot(i < CIT_NP && (g.pl[i < CIT_NP ? i : 0].flags & PF_CROWN));
+    const int fi = g.pl[i < CIT_NP ? i : 0].flags;
+    uint64_t m = cit_ballot((i < CIT_NP) & ((fi & PF_CROWN) != 0));
     c = m ? __ffsll((unsigned long long)m) - 1 : -1;
     if (c < 0) { g.err |= CIT_ERR_UNSUPPORTED; return; }
-    int v = i < CIT_NP ? g.turn[(i + c) % CIT_NP] : 0;    // every lane reads before any lane writes
+    int v = cit_ld(g.turn, (i + c) % CIT_NP, i < CIT_NP, 0);    // every lane reads before any lane writes
     if (i < CIT_NP) g.turn[i] = (uint8_t)v;
     gs_fresh(g, 0, cit_readlane(v, 0));
     kh_decay(g);
@@ -751,7 +756,7 @@ CIT_HD void cit_init_game(CitGame& g, CitMT& rng, bool preset) {
 #if CIT_WAVE
   {
     const int l = cit_lane();
-    int d0 = l < n ? g.deck[l] : 0, d1 = l + 64 < n ? g.deck[l + 64] : 0;
+    int d0 = cit_ld(g.deck, l, l < n, 0), d1 = l + 64 < n ? g.deck[l + 64] : 0;
     if (l < n) g.used_cards[l] = (uint8_t)d0;
     if (l + 64 < n && l + 64 < CIT_USED_CAP) g.used_cards[l + 64] = (uint8_t)d1;
   }
@@ -875,7 +880,20 @@ __device__ __forceinline__ CitOpt cit_readlane_opt(const CitOpt& o, int src) {
 }
 // true on the lowest valid lane of each key (the reference's `seen` sets:
 // first occurrence wins).  All lanes must be active.
+// One uniform iteration per distinct key: the lowest valid lane left takes its
+// key's whole ballot out of the set, so no lane leaves the loop early (no
+// exec-mask bookkeeping) and the count is the keys', not the lanes'.
 __device__ __forceinline__ bool cit_first_key(bool valid, int key) {
+#ifndef CIT_FIRST_KEY_LANES
+  uint64_t m = cit_ballot(valid), first = 0;
+  while (m) {
+    const int j = __ffsll((unsigned long long)m) - 1;
+    const int kj = __builtin_amdgcn_readlane(key, j);
+    m &= ~cit_ballot(valid && key == kj);   // j and every later lane with its key
+    first |= 1ull << j;
+  }
+  return (first >> cit_lane()) & 1;
+#else
   uint64_t m = cit_ballot(valid);
   int me = cit_lane();
   bool dup = false;
@@ -886,6 +904,7 @@ __device__ __forceinline__ bool cit_first_key(bool valid, int key) {
     dup |= key == __builtin_amdgcn_readlane(key, j);
   }
   return valid && !dup;
+#endif
 }
 // list sinks: proposals compacted into buf[n + rank]
 #define CIT_WAVE_LIST_EMIT                                        \
@@ -1235,7 +1254,8 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
 #if CIT_WAVE
       {
         int p = cit_lane();
-        WEMIT(p < CIT_NP && p != a && g.pl[p < CIT_NP ? p : 0].n_hand > 0, mk(O_LOOK_AT_HAND, a, p));
+        const int nhp = g.pl[p < CIT_NP ? p : 0].n_hand;
+        WEMIT((p < CIT_NP) & (p != a) & (nhp > 0), mk(O_LOOK_AT_HAND, a, p));
         return false;
       }
 #endif
@@ -1411,7 +1431,7 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
 #if CIT_WAVE
   {
     int i = cit_lane(), nh = P.n_hand;
-    WEMIT(i < nh, mk(O_LAB, a, -1, i < nh ? P.hand[i] : 0));
+    WEMIT(i < nh, mk(O_LAB, a, -1, cit_ld(P.hand, i, i < nh, 0)));
   }
 #else
     for (int i = 0; i < P.n_hand; i++) EMIT(mk(O_LAB, a, -1, P.hand[i]));
@@ -1428,7 +1448,7 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
 #if CIT_WAVE
       {
         int i = cit_lane(), nb = g.pl[p].n_build;
-        WEMIT(i < nb, mk(O_WEAPON_STORAGE, a, p, i < nb ? g.pl[p].build[i] : 0));
+        WEMIT(i < nb, mk(O_WEAPON_STORAGE, a, p, cit_ld(g.pl[p].build, i, i < nb, 0)));
       }
 #else
         for (int i = 0; i < g.pl[p].n_build; i++) EMIT(mk(O_WEAPON_STORAGE, a, p, g.pl[p].build[i]));
@@ -1446,7 +1466,7 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
   if (HAS(bm, 34) && !g.gs_adm[ADM_MUSEUM]) {
 #if CIT_WAVE
     int i = cit_lane(), nh = P.n_hand;
-    int c = i < nh ? P.hand[i] : 0;
+    int c = cit_ld(P.hand, i, i < nh, 0);
     WEMIT(cit_first_key(i < nh, card_type(c)), mk(O_MUSEUM, a, -1, c));
 #else
     uint64_t seen = 0;
@@ -1538,7 +1558,7 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
 #if CIT_WAVE
         if (nj <= 64) {
           int i = cit_lane();
-          int c = i < nj ? jd[i] : 0;
+          int c = cit_ld(jd, i, i < nj, 0);
           WEMIT(cit_first_key(i < nj, card_type(c)), mk(O_WHICH_CARD, a, -1, c, CIT_NO_CARD));
           return false;
         }
@@ -1829,7 +1849,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       {
         // turn_orders_for_roles is a permutation: one lane per seat
         int i = cit_lane();
-        int p = i < CIT_NP ? g.turn[i] : 0;
+        int p = cit_ld(g.turn, i, i < CIT_NP, 0);
         uint64_t at = cit_ballot(i < CIT_NP && p == a);
         int pos_a = at ? 63 - __clzll((long long)at) : 0;   // the last match, as the loop's
         if (i < CIT_NP && p != a) P.kr[p] = (uint16_t)((P.kr[p] & KR_CONFIRMED) | (i < pos_a ? before : rtc_mask));
@@ -1874,7 +1894,7 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       {
         int i = cit_lane(), nj = P.n_jd, nd = g.n_deck;
         if (nj <= 64 && nd + nj <= CIT_DECK_CAP - 1) {   // no overflow: one store by all lanes
-          int c = i < nj ? pl_jd(P)[i] : CIT_NO_CARD;
+          int c = cit_ld(pl_jd(P), i, i < nj, CIT_NO_CARD);
           bool v = i < nj && c != CIT_NO_CARD;
           uint64_t m = cit_ballot(v);
           if (v) deck_ref(g, nd + cit_lane_rank(m)) = (uint8_t)c;
@@ -2017,8 +2037,8 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
 #if CIT_WAVE
       {   // lane l holds both hands' cards l and l + 64 (area_splice calls src(l), src(l + 64) on lane l)
         const int l = cit_lane();
-        const int p0 = l < np ? P.hand[l] : 0, p1 = l + 64 < np ? P.hand[l + 64] : 0;
-        const int t0 = l < nt ? T.hand[l] : 0, t1 = l + 64 < nt ? T.hand[l + 64] : 0;
+        const int p0 = cit_ld(P.hand, l, l < np, 0), p1 = l + 64 < np ? P.hand[l + 64] : 0;
+        const int t0 = cit_ld(T.hand, l, l < nt, 0), t1 = l + 64 < nt ? T.hand[l + 64] : 0;
         area_splice(g, P, AL_HAND, 0, np, nt, [t0, t1](int i) { return i < 64 ? t0 : t1; });
         area_splice(g, T, AL_HAND, 0, nt, np, [p0, p1](int i) { return i < 64 ? p0 : p1; });
       }
@@ -2171,7 +2191,8 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
 #if CIT_WAVE
       {
         int l = cit_lane();
-        int gl = l < CIT_NP ? g.pl[l].gold : -32768;
+        int gl = g.pl[l < CIT_NP ? l : 0].gold;
+        gl = l < CIT_NP ? gl : -32768;
         int mx = __ockl_wfred_max_i32(gl);
         best = __ffsll((unsigned long long)cit_ballot(l < CIT_NP && gl == mx)) - 1;   // first maximum
       }
@@ -2294,7 +2315,10 @@ template <class Src, class Dst>
 CIT_HD int wave_append(Dst dst, int base, int cnt, Src src) {
   const int l = cit_lane();
   const uint64_t below = cit_below();
-  int c0 = l < cnt ? src(l) : CIT_NO_CARD, c1 = l + 64 < cnt ? src(l + 64) : CIT_NO_CARD;
+  // every lane calls src for its first element (each src reads in bounds past cnt): no
+  // branch around those loads; the second (past lane 64, rarely any) keeps its branch
+  int c0 = src(l), c1 = l + 64 < cnt ? src(l + 64) : CIT_NO_CARD;
+  c0 = l < cnt ? c0 : CIT_NO_CARD;
   uint64_t m0 = cit_ballot(c0 != CIT_NO_CARD), m1 = cit_ballot(c1 != CIT_NO_CARD);
   int n0 = __popcll(m0);
   if (c0 != CIT_NO_CARD) dst(base + __popcll(m0 & below)) = (uint8_t)c0;
@@ -2316,7 +2340,7 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
   const int nkh = g.n_kh;
   const int le = l < nkh ? l : 0;
   const int kowner = g.kh[le].owner, ktarget = g.kh[le].target, kflags = g.kh[le].conf_flags;
-  const int klen = l < nkh ? g.kh[le].len : 0;
+  const int klen = l < nkh ? (int)g.kh[le].len : 0;   // (le is clamped: an unconditional load)
   int koff = 0;
   for (int j = 0; j < nkh; j++) koff += j < l ? cit_readlane(klen, j) : 0;
   const bool mine = l < nkh && kowner == orig;
@@ -2367,7 +2391,7 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
   __syncthreads();
   const int nuc = g.n_used_cards;
   const bool v0 = l < nuc, v1 = l + 64 < nuc;
-  const int c0 = v0 ? g.used_cards[l] : 0, c1 = v1 ? g.used_cards[l + 64] : 0;
+  const int c0 = cit_ld(g.used_cards, l, v0, 0), c1 = v1 ? g.used_cards[l + 64] : 0;
   const int t0 = card_type(c0), t1 = card_type(c1);
   // rank among the earlier used cards of the same type: per-type masks of
   // the lanes holding that type (LDS atomic OR), popcount below this lane
@@ -2406,7 +2430,10 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
     int m = n < nu ? n : nu;
     // the known cards, then the shuffled unknowns: one compaction pass
     nd = wave_append(deck_slot, 0, kk + m,
-                     [&g, unk, lo, kk](int i) { return i < kk ? (int)g.kh_pool[lo + i] : (int)unk[i - kk]; });
+                     [&g, unk, lo, kk](int i) {
+                       const int a = g.kh_pool[i < kk ? lo + i : 0], b = unk[i < kk ? 0 : i - kk];
+                       return i < kk ? a : b;
+                     });
     head = m;
     g.n_deck = (uint8_t)nd;
   }
@@ -2436,7 +2463,7 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
   uint16_t kr[CIT_NP];
   for (int j = 0; j < CIT_NP; j++) kr[j] = PC.kr[j];
   // kr_strip: the role ids holding `role` as one ballot over lane r = roles[r]
-  const int rl = l < 8 ? g.roles[l] : ROLE_NONE;
+  const int rl = cit_ld(g.roles, l, l < 8, ROLE_NONE);
   auto strip = [&](int role) {
     uint16_t m = (uint16_t)(((uint32_t)cit_ballot(l < 8 && rl == role) << 1) | (role == ROLE_BEWITCHED ? 1u : 0u));
     for (int j = 0; j < CIT_NP; j++)
@@ -2469,7 +2496,8 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
       const int n_old = Q.n_hand;
       int nh = wave_append([&Q](int i) -> uint8_t& { return Q.hand[i < CIT_AREA_CAP ? i : 0]; }, 0, kk + m,
                            [&g, unk, ho, kk, head](int i) {
-                             return i < kk ? (int)g.kh_pool[ho + i] : (int)unk[head + i - kk];
+                             const int a = g.kh_pool[i < kk ? ho + i : 0], b = unk[i < kk ? 0 : head + i - kk];
+                             return i < kk ? a : b;
                            });
       head += m;
       if (nh < n_old) area_splice(g, Q, AL_HAND, nh, n_old - nh, 0, [](int) { return 0; });

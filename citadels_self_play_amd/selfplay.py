@@ -340,6 +340,8 @@ class TreeQueue:
             max_pool_bytes = int(0.8 * device_avail_bytes(dev))
         frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
         Q = max(1, int(per_round))
+        if slots and multi_round:
+            Q = max(Q, int(slots))      # a round-to-round queue may hold more trees than one round
         S = min(Q, slots or Q)
         while S > 1 and pool_bytes(S, node_cap, edge_cap, frac(S)) > max_pool_bytes:
             S = max(1, min(S - 1, int(max_pool_bytes // (pool_bytes(S, node_cap, edge_cap, frac(S)) / S))))

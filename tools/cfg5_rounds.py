@@ -23,12 +23,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--iters", type=int, default=200000)
     ap.add_argument("--seed", type=int, default=30_000_000 + 90 * 1_000_000)
+    ap.add_argument("--slots", type=int, default=0, help="queue slots (0: sized from one round)")
+    ap.add_argument("--overcommit", type=float, default=0.0, help="0: selfplay.QUEUE_OVERCOMMIT")
     a = ap.parse_args()
     msgs = []
     log = (lambda m: (msgs.append((round(time.perf_counter() - t0, 3), m)), print(m, file=sys.stderr, flush=True)))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    q = selfplay.TreeQueue(a.iters, a.trees, log=log)
+    q = selfplay.TreeQueue(a.iters, a.trees, log=log, slots=a.slots or None, overcommit=a.overcommit or None)
     t_init = time.perf_counter() - t0
     for r in range(a.rounds):
         q.add(selfplay.shard(a.trees, base_seed=a.seed + r * 1_000_000))

@@ -513,6 +513,45 @@ CIT_NOINLINE CfrCnt eng_list_upto2(CfrTree& T_in, int which) {
   cit_enum_options(g, s, cfr_glb(T.seer));
   return {s.n, s.err};
 }
+#if CIT_WAVE
+// eng_list_upto2 without the list: the count (a lower bound >= 2 once a second
+// option is known) and the first option, in registers.
+struct CfrFirst {
+  int n;
+  uint32_t err;
+  CitOpt o;
+};
+CIT_NOINLINE CfrFirst eng_first_upto2(CfrTree& T_in, int which) {
+  CIT_PROF_SCOPE(2);
+  CfrTree& T = CFR_T(T_in);
+  const CitGame& g = cfr_w(T, cfr_u(which));
+  Upto2FirstSink s(cfr_u(cit_enum_late_error(g) ? 0 : 1) != 0);
+  cit_enum_options(g, s, cfr_glb(T.seer));
+  return {s.n, s.err, s.first};
+}
+// eng_list_lds with the list in registers (RegSink: lane i holds option i of
+// the first 64); the draw reads its option with readlanes.
+struct CfrRegList {
+  int n;
+  uint32_t err;
+  uint32_t r0, r1, r2, r3;
+};
+CIT_NOINLINE CfrRegList eng_list_reg(CfrTree& T_in, int which) {
+  CIT_PROF_SCOPE(2);
+  CfrTree& T = CFR_T(T_in);
+  RegSink s;
+  cit_enum_options(cfr_w(T, cfr_u(which)), s, cfr_glb(T.seer));
+  return {s.n, s.err, s.r0, s.r1, s.r2, s.r3};
+}
+__device__ __forceinline__ CitOpt cfr_reg_opt(const CfrRegList& L, int k) {
+  RegSink s;
+  s.r0 = L.r0;
+  s.r1 = L.r1;
+  s.r2 = L.r2;
+  s.r3 = L.r3;
+  return s.at(k);
+}
+#endif
 CIT_NOINLINE void eng_sample(CfrTree& T_in, int which, int orig, int role_sample) {
   CIT_PROF_SCOPE(5);
   CfrTree& T = CFR_T(T_in);
@@ -934,6 +973,30 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
   int n = 0;
   {
   CIT_PROF_SCOPE(21);                  // skip_false_choice
+#if CIT_WAVE
+  // the count and the first option come back in registers (no LDS list)
+  CitOpt first = mk(O_NUM_NAMES, 0);
+  if (!cfr_u(skipped)) {
+    eng_prepare(T, which);
+    CfrFirst c = eng_first_upto2(T, which);
+    n = cfr_u(c.n);
+    e |= cfr_u(c.err);
+    first = cfr_uopt(c.o);
+  }
+  int i = 0;
+  bool done = false;
+  while (n == 1 && !done && !e && !w.err) {
+    i++;
+    int win = cfr_u(eng_carry(T, which, first));
+    done = win >= 0;
+    eng_prepare(T, which);
+    CfrFirst c = eng_first_upto2(T, which);
+    n = cfr_u(c.n);
+    e |= cfr_u(c.err);
+    first = cfr_uopt(c.o);
+    if (i > 100) done = true;
+  }
+#else
   if (!cfr_u(skipped)) {
     eng_prepare(T, which);
     CfrCnt c = cfr_ucnt(eng_list_upto2(T, which));
@@ -953,6 +1016,7 @@ CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int s
     e |= c.err;
     if (i > 100) done = true;
   }
+#endif
   }
   T.err |= e | w.err;
   if (T.n_nodes >= T.node_cap) { T.err |= CIT_ERR_OVERFLOW | CIT_ERR_POOL_CAP; return -1; }
@@ -1064,11 +1128,20 @@ CIT_NOINLINE void cfr_expand_role_pick(CfrTree& T_in, int n, int depth) {
     int guard = 0;
     while (h.gs_state != 1 && !T.err) {
       eng_prepare(T, 1);
+#if CIT_WAVE
+      const CfrRegList c = eng_list_reg(T, 1);
+      const int cn = cfr_u(c.n);
+      T.err |= cfr_u(c.err);
+      int k = cfr_with_np(T, [&](CitMT& r_) { return np_choice_uniform(r_, cn, T.err); });
+      if (T.err) break;
+      last = k < 64 ? cfr_uopt(cfr_reg_opt(c, k)) : cfr_uopt(eng_pick(T, 1, k));
+#else
       CfrCnt c = cfr_ucnt(eng_list_lds(T, 1));
       T.err |= c.err;
       int k = cfr_with_np(T, [&](CitMT& r_) { return np_choice_uniform(r_, c.n, T.err); });
       if (T.err) break;
       last = k < CFR_LBUF ? cfr_uopt(cfr_lbuf(T)[k]) : cfr_uopt(eng_pick(T, 1, k));
+#endif
       eng_carry(T, 1, last);
       T.err |= h.err;
       if (++guard > 64) T.err |= CIT_ERR_UNSUPPORTED;
@@ -1170,11 +1243,20 @@ CIT_NOINLINE void cfr_expand_opponent(CfrTree& T_in, int n, int par, int player,
   CitGame& h = cfr_w(T, 1);
   if (par < 0 || player != pp) eng_sample(T, 1, T.orig, par >= 0 && ps != 0);
   eng_prepare(T, 1);
+#if CIT_WAVE
+  const CfrRegList lc = eng_list_reg(T, 1);
+  const int ln = cfr_u(lc.n);
+  T.err |= cfr_u(lc.err) | h.err;
+  int k = cfr_with_np(T, [&](CitMT& r_) { return np_choice_uniform(r_, ln, T.err); });
+  if (T.err) return;
+  CitOpt o = k < 64 ? cfr_uopt(cfr_reg_opt(lc, k)) : cfr_uopt(eng_pick(T, 1, k));
+#else
   CfrCnt lc = cfr_ucnt(eng_list_lds(T, 1));
   T.err |= lc.err | h.err;
   int k = cfr_with_np(T, [&](CitMT& r_) { return np_choice_uniform(r_, lc.n, T.err); });
   if (T.err) return;
   CitOpt o = k < CFR_LBUF ? cfr_uopt(cfr_lbuf(T)[k]) : cfr_uopt(eng_pick(T, 1, k));
+#endif
   opt_mutate(o, h);
   CitOpt key = opt_key(o, h);
   eng_carry(T, 1, o);

@@ -1100,6 +1100,34 @@ struct Upto2Sink {
 #endif
 };
 
+#if CIT_WAVE
+// Upto2Sink keeping only the first option, wave-uniform (skip_false_choice
+// carries it out when it is the only one): no list in LDS.
+struct Upto2FirstSink {
+  int n = 0;
+  uint32_t err = 0;
+  bool stop;
+  CitOpt first;
+  __device__ explicit Upto2FirstSink(bool s) : stop(s) {}
+  __device__ bool emit(const CitOpt& o) {
+    if (n == 0) first = o;
+    n++;
+    return stop && n >= 2;
+  }
+  template <class F> __device__ bool block(int cnt, F&& f) {
+    if (n == 0 && cnt > 0) first = f(0);
+    n += cnt;
+    return stop && n >= 2;
+  }
+  __device__ bool wave_emit(bool p, const CitOpt& o) {
+    const uint64_t m = cit_ballot(p);
+    if (n == 0 && m) first = cit_readlane_opt(o, __ffsll((unsigned long long)m) - 1);
+    n += __popcll(m);
+    return stop && n >= 2;
+  }
+};
+#endif
+
 #define EMIT(...)                                  \
   do {                                             \
     if (s.emit(__VA_ARGS__)) return true;          \

@@ -67,7 +67,11 @@ MLPW_HD constexpr long mlpw_floats(int K, int N) { return (long)K * mlpw_rs(N); 
 #define MLPW_R_H3 0
 #define MLPW_R_LOGITS 768
 #define MLPW_R_PROBS 776
-#define MLPW_R_FLOATS 932
+// the layer's non-zero inputs as a u16 list (<= 512 entries + the ring's
+// look-ahead pad), after x: 544 u16 = 272 floats
+#define MLPW_R_LIST 932
+#define MLPW_LIST_CAP 544
+#define MLPW_R_FLOATS (MLPW_R_LIST + MLPW_LIST_CAP / 2)
 
 // Element e of the row layout of W [K][N] (row-major, k major).
 MLPW_HD inline float mlpw_pack_elem(const float* W, int K, int N, long e) {
@@ -239,6 +243,104 @@ __device__ __forceinline__ void mlpw_layer(const float* Wl, const float* bias, c
   }
 }
 
+#ifndef MLPW_LIST
+#define MLPW_LIST 1
+#endif
+typedef __attribute__((address_space(3))) uint16_t mlpw_lds_u16;
+typedef unsigned mlpw_u2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) mlpw_u2 mlpw_lds_u2;
+// The same layer driven by a list instead of the mask cursor: the non-zero
+// inputs, ascending, are compacted once into a u16 list in LDS (one ballot
+// per 64 inputs), and the ring reads the list four entries at a time, four
+// steps ahead of the rows it issues -- a step is then a row address, two
+// loads and the FMAs (the cursor's ~30 scalar instructions per row gone).
+// The list is padded with row 0 past its end, so the look-ahead never
+// issues a load outside the layer.  Same inputs in the same order: the
+// chains are the cursor's, bit for bit.
+template <int K, int N, int PF, bool RELU>
+__device__ __forceinline__ void mlpw_layer_list(const float* Wl, const float* bias, const mlpw_lds_t* x, bool skip,
+                                                mlpw_lds_u16* list, mlpw_lds_t* y) {
+  static_assert(PF % 4 == 0 && K + PF + 8 <= MLPW_LIST_CAP, "list look-ahead");
+  constexpr int S = N >= 64 ? N / 64 : 1;
+  const int lane = __lane_id();
+  const uint64_t below = (1ull << lane) - 1;
+  int nnz = 0;
+#pragma unroll
+  for (int i = 0; i < K; i += 64) {
+    const int k = i + lane;
+    const float xv = x[k < K ? k : 0];
+    const bool nz = k < K && (!skip || xv != 0.0f);
+    const uint64_t m = __ballot(nz);
+    if (nz) list[nnz + __popcll(m & below)] = (uint16_t)k;
+    nnz += __popcll(m);
+  }
+  nnz = __builtin_amdgcn_readfirstlane(nnz);
+  if (lane < PF + 8) list[nnz + lane] = 0;
+  const __attribute__((address_space(1))) char* wb = (const __attribute__((address_space(1))) char*)mlpw_glb(Wl);
+  const uint32_t voff = (uint32_t)(N >= 64 ? lane * S : (lane < N ? lane : N - 1)) * 4u;
+  const mlpw_lds_u2* l4 = (const mlpw_lds_u2*)list;          // four entries per 8-byte read
+  float acc[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) acc[s] = 0.0f;
+  mlpw_row<S> w[PF];
+  float xr[PF];
+  auto entry = [](mlpw_u2 q, int j) {
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)(j < 2 ? q.x : q.y));
+    return (int)((j & 1) ? (v >> 16) : (v & 0xffffu));
+  };
+#pragma unroll
+  for (int i = 0; i < PF; i += 4) {
+    const mlpw_u2 q = l4[i / 4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int k = entry(q, j);
+      w[i + j] = mlpw_ld<N>(wb, k, voff);
+      xr[i + j] = x[k];
+    }
+  }
+  mlpw_u2 q0 = l4[PF / 4], q1 = l4[PF / 4 + 1];   // the next eight entries to issue (read 4 steps ahead)
+  auto step = [&](int i, int t) {        // t: the step's list position (t % 4 == i % 4)
+    const float xv = xr[i];
+    if constexpr (S == 1) {
+      acc[0] = __builtin_fmaf(xv, w[i].v[0], acc[0]);
+    } else {
+      const mlpw_f2 xx = mlpw_f2{xv, xv};
+#pragma unroll
+      for (int s = 0; s < S; s += 2) {
+        const mlpw_f2 r = __builtin_elementwise_fma(xx, mlpw_f2{w[i].v[s], w[i].v[s + 1]},
+                                                    mlpw_f2{acc[s], acc[s + 1]});
+        acc[s] = r.x;
+        acc[s + 1] = r.y;
+      }
+    }
+    const int k = entry(q0, i & 3);      // refill the slot with entry t + PF
+    w[i] = mlpw_ld<N>(wb, k, voff);
+    xr[i] = x[k];
+    if ((i & 3) == 3) {                  // entries t + PF + 5 .. t + PF + 8, used four steps on
+      q0 = q1;
+      q1 = l4[(t + PF + 5) / 4];
+    }
+  };
+  const int full = nnz - nnz % PF;
+#pragma nounroll
+  for (int t0 = 0; t0 < full; t0 += PF) {
+#pragma unroll
+    for (int i = 0; i < PF; i++) step(i, t0 + i);
+  }
+#pragma unroll
+  for (int i = 0; i < PF - 1; i++)
+    if (i < nnz - full) step(i, full + i);
+  mlpw_gf_t* bp = mlpw_glb(bias);
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const int c = N >= 64 ? 64 * s + lane : lane;
+    if (c < N) {
+      const float v = acc[s] + bp[c];
+      y[c] = RELU ? (v > 0.0f ? v : 0.0f) : v;
+    }
+  }
+}
+
 // The forward over the row at R + MLPW_R_X (MLPW_IN floats) with the
 // row-layout weights Q: logits to R + MLPW_R_LOGITS, probabilities
 // (square_and_normalize, the sum in index order) to R + MLPW_R_PROBS.  The
@@ -247,6 +349,17 @@ __device__ __forceinline__ void mlpw_layer(const float* Wl, const float* bias, c
 __device__ __forceinline__ void mlpw_forward(const float* Q, mlpw_lds_t* R) {
   const bool skip = *(const __attribute__((address_space(1))) uint32_t*)(mlpw_glb(Q) + MLPW_FLAG) != 0u;
   __syncthreads();
+#if MLPW_LIST
+  mlpw_lds_u16* list = (mlpw_lds_u16*)(R + MLPW_R_LIST);
+  mlpw_layer_list<MLPW_IN, MLPW_H1, 8, true>(Q + MLPW_L1, Q + MLPW_B1, R + MLPW_R_X, skip, list, R + MLPW_R_H1);
+  __syncthreads();
+  mlpw_layer_list<MLPW_H1, MLPW_H2, 12, true>(Q + MLPW_L2, Q + MLPW_B2, R + MLPW_R_H1, skip, list, R + MLPW_R_H2);
+  __syncthreads();
+  mlpw_layer_list<MLPW_H2, MLPW_H3, 16, true>(Q + MLPW_L3, Q + MLPW_B3, R + MLPW_R_H2, skip, list, R + MLPW_R_H3);
+  __syncthreads();
+  mlpw_layer_list<MLPW_H3, MLPW_OUT, 16, false>(Q + MLPW_L4, Q + MLPW_B4, R + MLPW_R_H3, skip, list, R + MLPW_R_LOGITS);
+  __syncthreads();
+#else
   MlpwMask M = mlpw_mask<MLPW_IN>(R + MLPW_R_X, skip);
   mlpw_layer<MLPW_IN, MLPW_H1, 8, true>(Q + MLPW_L1, Q + MLPW_B1, R + MLPW_R_X, M, R + MLPW_R_H1);
   __syncthreads();
@@ -259,6 +372,7 @@ __device__ __forceinline__ void mlpw_forward(const float* Q, mlpw_lds_t* R) {
   M = mlpw_mask<MLPW_H3>(R + MLPW_R_H3, skip);
   mlpw_layer<MLPW_H3, MLPW_OUT, 16, false>(Q + MLPW_L4, Q + MLPW_B4, R + MLPW_R_H3, M, R + MLPW_R_LOGITS);
   __syncthreads();
+#endif
   float sq[MLPW_OUT], s = 0.0f;
 #pragma unroll
   for (int j = 0; j < MLPW_OUT; j++) {

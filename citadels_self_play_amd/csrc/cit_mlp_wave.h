@@ -246,6 +246,19 @@ __device__ __forceinline__ void mlpw_layer(const float* Wl, const float* bias, c
 #ifndef MLPW_LIST
 #define MLPW_LIST 1
 #endif
+// rows in flight per layer (multiples of 4; a layer-1 row is 8 VGPRs a lane)
+#ifndef MLPW_PF1
+#define MLPW_PF1 8
+#endif
+#ifndef MLPW_PF2
+#define MLPW_PF2 12
+#endif
+#ifndef MLPW_PF3
+#define MLPW_PF3 16
+#endif
+#ifndef MLPW_PF4
+#define MLPW_PF4 16
+#endif
 typedef __attribute__((address_space(3))) uint16_t mlpw_lds_u16;
 typedef unsigned mlpw_u2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) mlpw_u2 mlpw_lds_u2;
@@ -351,13 +364,13 @@ __device__ __forceinline__ void mlpw_forward(const float* Q, mlpw_lds_t* R) {
   __syncthreads();
 #if MLPW_LIST
   mlpw_lds_u16* list = (mlpw_lds_u16*)(R + MLPW_R_LIST);
-  mlpw_layer_list<MLPW_IN, MLPW_H1, 8, true>(Q + MLPW_L1, Q + MLPW_B1, R + MLPW_R_X, skip, list, R + MLPW_R_H1);
+  mlpw_layer_list<MLPW_IN, MLPW_H1, MLPW_PF1, true>(Q + MLPW_L1, Q + MLPW_B1, R + MLPW_R_X, skip, list, R + MLPW_R_H1);
   __syncthreads();
-  mlpw_layer_list<MLPW_H1, MLPW_H2, 12, true>(Q + MLPW_L2, Q + MLPW_B2, R + MLPW_R_H1, skip, list, R + MLPW_R_H2);
+  mlpw_layer_list<MLPW_H1, MLPW_H2, MLPW_PF2, true>(Q + MLPW_L2, Q + MLPW_B2, R + MLPW_R_H1, skip, list, R + MLPW_R_H2);
   __syncthreads();
-  mlpw_layer_list<MLPW_H2, MLPW_H3, 16, true>(Q + MLPW_L3, Q + MLPW_B3, R + MLPW_R_H2, skip, list, R + MLPW_R_H3);
+  mlpw_layer_list<MLPW_H2, MLPW_H3, MLPW_PF3, true>(Q + MLPW_L3, Q + MLPW_B3, R + MLPW_R_H2, skip, list, R + MLPW_R_H3);
   __syncthreads();
-  mlpw_layer_list<MLPW_H3, MLPW_OUT, 16, false>(Q + MLPW_L4, Q + MLPW_B4, R + MLPW_R_H3, skip, list, R + MLPW_R_LOGITS);
+  mlpw_layer_list<MLPW_H3, MLPW_OUT, MLPW_PF4, false>(Q + MLPW_L4, Q + MLPW_B4, R + MLPW_R_H3, skip, list, R + MLPW_R_LOGITS);
   __syncthreads();
 #else
   MlpwMask M = mlpw_mask<MLPW_IN>(R + MLPW_R_X, skip);

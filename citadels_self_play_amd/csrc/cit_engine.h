@@ -1169,13 +1169,18 @@ CIT_HD uint64_t unrank_comb(int n, int k, long idx) {
 template <class S>
 CIT_HD bool gen_builds(const CitGame& g, int a, uint64_t bm, S& s) {
   const CitPlayer& P = g.pl[a];
-  int lim = P.role == R_ARCHITECT ? 3 : P.role == R_SCHOLAR ? 2 : (P.role == R_BISHOP || P.role == R_NAVIGATOR) ? 0 : 1;
-  int done = g.gs_adm[ADM_NON_TRADE] + (P.role == R_TRADER ? 0 : g.gs_adm[ADM_TRADE]);
+  const int role = P.role, adm_nt = g.gs_adm[ADM_NON_TRADE], adm_tr = g.gs_adm[ADM_TRADE];
+#if CIT_WAVE
+  const int nh = P.n_hand, gold = P.gold, reps = P.replicas;   // loaded with the role: one round trip
+  __asm__ volatile("" ::"v"(role), "v"(adm_nt), "v"(adm_tr), "v"(nh), "v"(gold), "v"(reps));
+#endif
+  int lim = role == R_ARCHITECT ? 3 : role == R_SCHOLAR ? 2 : (role == R_BISHOP || role == R_NAVIGATOR) ? 0 : 1;
+  int done = adm_nt + (role == R_TRADER ? 0 : adm_tr);
   if (done >= lim) return false;
   bool factory = HAS(bm, 35);
 #if CIT_WAVE
   {
-    int i = cit_lane(), nh = P.n_hand, gold = P.gold, reps = P.replicas;
+    int i = cit_lane();
     int c = 0, t = 0;
     bool q = false;
     if (i < nh) {
@@ -1447,15 +1452,34 @@ CIT_HD bool gen_role(const CitGame& g, int a, S& s) {
 template <class S>
 CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
   const CitPlayer& P = g.pl[a];
-  const uint64_t bm = type_mask(P.build, P.n_build);
-  if (gen_builds(g, a, bm, s)) return true;
-  if (!g.gs_adm[ADM_ABILITY])
-    if (gen_role(g, a, s)) return true;
-  if (P.role == R_ABBOT && !g.gs_adm[ADM_BEGGED]) EMIT(mk(O_ABBOT_BEG, a));
-  if ((P.role == R_WARLORD || P.role == R_MARSHAL || P.role == R_DIPLOMAT) && !g.gs_adm[ADM_TAKE_GOLD])
+  uint64_t bm;
+  {
+    CIT_PROF_SCOPE(25);
+    bm = type_mask(P.build, P.n_build);
+  }
+  {
+    CIT_PROF_SCOPE(26);
+    if (gen_builds(g, a, bm, s)) return true;
+  }
+  {
+    CIT_PROF_SCOPE(27);
+    if (!g.gs_adm[ADM_ABILITY])
+      if (gen_role(g, a, s)) return true;
+  }
+  CIT_PROF_SCOPE(28);
+  // the fields the remaining tests read, in one round of loads
+  const int role = P.role, gold = P.gold, pfl = P.flags;
+  const int adm_beg = g.gs_adm[ADM_BEGGED], adm_tg = g.gs_adm[ADM_TAKE_GOLD], adm_sm = g.gs_adm[ADM_SMITHY],
+            adm_lab = g.gs_adm[ADM_LAB], adm_ms = g.gs_adm[ADM_MAGIC_SCHOOL], adm_mu = g.gs_adm[ADM_MUSEUM];
+#if CIT_WAVE
+  __asm__ volatile("" ::"v"(role), "v"(gold), "v"(pfl), "v"(adm_beg), "v"(adm_tg), "v"(adm_sm), "v"(adm_lab),
+                   "v"(adm_ms), "v"(adm_mu));
+#endif
+  if (role == R_ABBOT && !adm_beg) EMIT(mk(O_ABBOT_BEG, a));
+  if ((role == R_WARLORD || role == R_MARSHAL || role == R_DIPLOMAT) && !adm_tg)
     EMIT(mk(O_TAKE_GOLD_WAR, a));
-  if (HAS(bm, 21) && P.gold >= 2 && !g.gs_adm[ADM_SMITHY]) EMIT(mk(O_SMITHY, a));
-  if (HAS(bm, 22) && !g.gs_adm[ADM_LAB])
+  if (HAS(bm, 21) && gold >= 2 && !adm_sm) EMIT(mk(O_SMITHY, a));
+  if (HAS(bm, 22) && !adm_lab)
 #if CIT_WAVE
   {
     int i = cit_lane(), nh = P.n_hand;
@@ -1464,7 +1488,7 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
 #else
     for (int i = 0; i < P.n_hand; i++) EMIT(mk(O_LAB, a, -1, P.hand[i]));
 #endif
-  if (!g.gs_adm[ADM_MAGIC_SCHOOL] && HAS(bm, 25))
+  if (!adm_ms && HAS(bm, 25))
 #if CIT_WAVE
     WEMIT(cit_lane() < 5, mk(O_MAGIC_SCHOOL, a, -1, cit_lane()));
 #else
@@ -1481,7 +1505,7 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
 #else
         for (int i = 0; i < g.pl[p].n_build; i++) EMIT(mk(O_WEAPON_STORAGE, a, p, g.pl[p].build[i]));
 #endif
-  if (HAS(bm, 29) && (P.flags & PF_LIGHTHOUSE)) {
+  if (HAS(bm, 29) && (pfl & PF_LIGHTHOUSE)) {
     uint64_t seen = 0;
     for (int i = 0; i < g.n_deck; i++) {
       int c = deck_at(g, i), t = card_type(c);
@@ -1491,7 +1515,7 @@ CIT_HD bool gen_main(const CitGame& g, int a, S& s) {
       }
     }
   }
-  if (HAS(bm, 34) && !g.gs_adm[ADM_MUSEUM]) {
+  if (HAS(bm, 34) && !adm_mu) {
 #if CIT_WAVE
     int i = cit_lane(), nh = P.n_hand;
     int c = cit_ld(P.hand, i, i < nh, 0);
@@ -1551,6 +1575,14 @@ CIT_HD bool gen_wizard_take(const CitGame& g, int a, S& s) {
 // get_options dispatcher (agent.py:50-83) on a prepared game.
 template <class S>
 CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
+  CIT_PROF_SCOPE(29);
+#if CIT_WAVE
+  // the mover, the state, every seat's role (lane p) and every role's
+  // properties (lane r) in one round of loads: the role and its properties
+  // are then readlanes, not loads behind the mover's id
+  const int l_ = cit_lane();
+  const int prole_ = g.pl[l_ < CIT_NP ? l_ : 0].role, prp_ = g.rp[l_ & 7];
+#endif
   int a = g.gs_pid;
   if (a < 0 || a >= CIT_NP) { s.err |= CIT_ERR_UNSUPPORTED; return true; }
   const CitPlayer& P = g.pl[a];
@@ -1564,12 +1596,21 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
       if ((g.rtc >> r) & 1) EMIT(mk(O_ROLE_PICK, a, -1, r));
     return false;
   }
+#if CIT_WAVE
+  int role = cit_readlane(prole_, a);
+#else
   int role = P.role;
+#endif
   bool crown = role == R_KING || role == R_PATRICIAN;
   bool bew = role == ROLE_BEWITCHED;
   if (!bew && role >= 27) { s.err |= CIT_ERR_KEY; return true; }
   int rk = bew ? -1 : role / 3;
-  if (bew || !(g.rp[rk] & RP_DEAD)) {
+#if CIT_WAVE
+  const int rp_rk = bew ? 0 : cit_readlane(prp_, rk);
+#else
+  const int rp_rk = bew ? 0 : g.rp[rk];
+#endif
+  if (bew || !(rp_rk & RP_DEAD)) {
     switch (st) {
       case 1:
         EMIT(mk(O_GOLD_OR_CARD, a, -1, 0));
@@ -1603,7 +1644,7 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
       }
       case 3:
         if (bew) { s.err |= CIT_ERR_KEY; return true; }
-        if (rp_blackmail(g.rp[rk])) {
+        if (rp_blackmail(rp_rk)) {
           EMIT(mk(O_BLACKMAIL_RESPONSE, a, -1, 0));
           EMIT(mk(O_BLACKMAIL_RESPONSE, a, -1, 1));
         } else {
@@ -1632,7 +1673,7 @@ CIT_HD bool cit_enum_options(const CitGame& g, S& s, const uint64_t* seer) {
       return false;
     }
     if (bew) { s.err |= CIT_ERR_KEY; return true; }
-    if (!(g.rp[rk] & RP_POSSESSED)) {
+    if (!(rp_rk & RP_POSSESSED)) {
       switch (st) {
         case 5:
           return gen_main(g, a, s);
@@ -1852,10 +1893,12 @@ CIT_HD int do_finish(CitGame& g, const CitOpt& o, CitMT& rng) {
   }
   if (g.n_used_roles == 0 || g.n_used_roles == 255) { g.err |= CIT_ERR_INDEX; return -1; }
   if (g.used_roles[g.n_used_roles - 1] == role_rank(g, P.role)) {
+    CIT_PROF_SCOPE(30);
     int w = check_game_ending(g);
     if (w < 0) cit_setup_round(g, rng);
     return w;
   }
+  CIT_PROF_SCOPE(31);
   setup_next_player(g, a);
   return -1;
 }

@@ -290,12 +290,18 @@ __global__ void k_random_choice(uint32_t* games, uint32_t* mt, uint32_t* idx, in
 // LDS stores.  (HW_REG_SHADER_CYCLES reads 0 on gfx950.)
 __device__ __forceinline__ unsigned long long prof_clk() { return clock64(); }
 __device__ __forceinline__ unsigned long long prof_d(unsigned long long a, unsigned long long b) { return b - a; }
-__device__ int prof_step(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* buf, int cap, unsigned long long* acc) {
+__device__ __forceinline__ int prof_step(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* buf, int cap, unsigned long long* acc) {
   int st = g.gs_state;
   unsigned long long t0c = prof_clk();
   cit_prepare_options(g, rng, seer);
   unsigned long long t1 = prof_clk();
+#if CIT_WAVE
+  RegSink s;                               // the default step's sink (ROLLOUT_REG)
+  (void)buf;
+  (void)cap;
+#else
   BufSink s(buf, cap);
+#endif
   cit_enum_options(g, s, seer);
   unsigned long long t2 = prof_clk();
   if (s.err) { g.err |= s.err; return 1; }
@@ -303,7 +309,11 @@ __device__ int prof_step(CitGame& g, CitMT& rng, uint64_t* seer, CitOpt* buf, in
   if (n == 0) { g.err |= CIT_ERR_EMPTY; return 1; }
   int k = (int)mt_randbelow(rng, (uint32_t)n);
   unsigned long long t3 = prof_clk();
+#if CIT_WAVE
+  CitOpt o = k < 64 ? s.at(k) : cit_pick_option(g, k, seer);
+#else
   CitOpt o = k < cap ? buf[k] : cit_pick_option(g, k, seer);
+#endif
   unsigned long long t4 = prof_clk();
   int w = cit_carry_out(g, o, rng);
   unsigned long long t5 = prof_clk();
@@ -334,6 +344,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROLL_WAVES_P
 #ifdef ROLL_CLOCK
   unsigned long long rc0 = wall_clock64();
 #endif
+  cfr_prof_reset();                         // (CIT_PROF builds: the engine scopes of this game)
   uniform_game<true, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
     uint64_t* sc = seer + l * CIT_SEER_MAX;
     int cap = max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps;
@@ -364,6 +375,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ROLL_WAVES_P
     g_roll_clock[2 * blockIdx.x + 1] = wall_clock64();
   }
 #endif
+  cfr_prof_flush();
 }
 
 // The same rollout as a work queue (cit_rollout_queue): a grid of as many
@@ -470,6 +482,17 @@ int cit_roll_prof_read(unsigned long long* out) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_roll_prof), sizeof(unsigned long long) * 160);
   unsigned long long z[160] = {};
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_roll_prof), z, sizeof(z));
+  return (int)e;
+}
+#endif
+
+#ifdef CIT_PROF
+// the engine's CIT_PROF_SCOPE sums of this unit's rollouts (then cleared):
+// [i] cycles, [32 + i] calls of scope i (tools/prof_rollout_scopes.py)
+int cit_hip_prof_read(unsigned long long* out) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cit_prof), sizeof(unsigned long long) * 64);
+  unsigned long long z[64] = {};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_cit_prof), z, sizeof(z));
   return (int)e;
 }
 #endif

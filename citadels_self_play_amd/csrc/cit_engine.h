@@ -1865,6 +1865,34 @@ CIT_HD void settle(CitGame& g, int name, int a, int t, int card) {
 CIT_HD int do_finish(CitGame& g, const CitOpt& o, CitMT& rng) {
   int a = o.perp;
   CitPlayer& P = g.pl[a];
+#if CIT_WAVE
+  // the tests below read one round of loads: the mover's role, hand size
+  // and buildings (lane i), every role's properties (lane r), the used roles
+  // (lane k) and the error word
+  const int l_ = cit_lane();
+  const int role_ = P.role, nh_ = P.n_hand, nb_ = P.n_build, bl_ = P.build[l_ & (CIT_BUILD_CAP - 1)];
+  const int rpl_ = g.rp[l_ & 7], nu_ = g.n_used_roles, url_ = g.used_roles[l_ < CIT_NP ? l_ : 0];
+  const uint32_t err_ = g.err;
+  __asm__ volatile("" ::"v"(role_), "v"(nh_), "v"(nb_), "v"(bl_), "v"(rpl_), "v"(nu_), "v"(url_), "v"(err_));
+  // rp_of(g, P.role): role_rank's KeyError (role >= 27, not Bewitched) and
+  // rp_of's (Bewitched) are together "role >= 27", the dict then read at 0
+  const bool key_ = role_ >= 27;
+  if (key_) g.err = err_ | CIT_ERR_KEY;
+  const bool dead = (cit_readlane(rpl_, key_ ? 0 : role_ / 3) & RP_DEAD) != 0;
+  if (err_ || key_) return -1;
+  if (!dead && nh_ == 0) {   // (just-drawn cards leave the hand size as it is)
+    const bool h28 = cit_ballot((l_ < nb_) & (card_type(bl_) == 28)) != 0;
+    const bool h30 = cit_ballot((l_ < nb_) & (card_type(bl_) == 30)) != 0;
+    if (h28) pl_draw(g, rng, P, AL_JD, 2);
+    if (h30) P.gold++;
+  }
+  if (o.flags & OF_CROWN) {
+    confirm_roles(g, a);
+    move_crown(g, a);
+  } else if (dead) {
+    confirm_roles(g, a);
+  }
+#else
   bool dead = rp_of(g, P.role) & RP_DEAD;
   if (g.err) return -1;
   if (!dead && P.n_hand == 0) {     // (the reference tests the building first; both tests are pure)
@@ -1877,6 +1905,7 @@ CIT_HD int do_finish(CitGame& g, const CitOpt& o, CitMT& rng) {
   } else if (rp_of(g, P.role) & RP_DEAD) {
     confirm_roles(g, a);
   }
+#endif
   if (o.flags & OF_NEXT_WITCH) {
     int w = holder_checked(g, 0);
     gs_set(g, 5, w);
@@ -1891,8 +1920,14 @@ CIT_HD int do_finish(CitGame& g, const CitOpt& o, CitMT& rng) {
     gs_rebind_adm(g);
     return -1;
   }
+#if CIT_WAVE
+  if (nu_ == 0 || nu_ == 255) { g.err |= CIT_ERR_INDEX; return -1; }
+  const int last_ = nu_ - 1 < CIT_NP ? cit_readlane(url_, nu_ - 1) : (int)g.used_roles[nu_ - 1];
+  if (last_ == role_ / 3) {                      // (role_ < 27 here: role_rank is role / 3)
+#else
   if (g.n_used_roles == 0 || g.n_used_roles == 255) { g.err |= CIT_ERR_INDEX; return -1; }
   if (g.used_roles[g.n_used_roles - 1] == role_rank(g, P.role)) {
+#endif
     CIT_PROF_SCOPE(30);
     int w = check_game_ending(g);
     if (w < 0) cit_setup_round(g, rng);

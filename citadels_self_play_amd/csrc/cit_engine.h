@@ -1978,6 +1978,32 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
       break;
     }
     case O_GOLD_OR_CARD: {                                   // :33-55
+#if CIT_WAVE
+      {   // one round of loads: role, gold, buildings (lane i), every role's properties (lane r)
+        const int l = cit_lane();
+        const int role = P.role, gold = P.gold, nb = P.n_build, bl = P.build[l & (CIT_BUILD_CAP - 1)];
+        const int rpl = g.rp[l & 7];
+        __asm__ volatile("" ::"v"(role), "v"(gold), "v"(nb), "v"(bl), "v"(rpl));
+        // confirm_roles(g, a) then rp_of(g, P.role): KeyError iff role >= 27
+        const int rq = role == ROLE_BEWITCHED ? -1 : role >= 27 ? 0 : role / 3;
+        if (role >= 27) g.err |= CIT_ERR_KEY;
+        if (l < CIT_NP) g.pl[l].kr[a] = (uint16_t)((1u << (rq + 1)) | KR_CONFIRMED);
+        if (cit_readlane(rpl, role >= 27 ? 0 : role / 3) & RP_ROBBED) {
+          int th = holder_checked(g, 1);
+          g.pl[th].gold = (int16_t)(g.pl[th].gold + gold);
+          P.gold = 0;
+        }
+        if (o.a == 0) {
+          P.gold += 2;
+          gs_set(g, 3, a);
+        } else {
+          const bool h16 = cit_ballot((l < nb) & (card_type(bl) == 16)) != 0;
+          pl_draw(g, rng, P, AL_JD, h16 ? 3 : 2);
+          gs_set(g, 2, a);
+        }
+        break;
+      }
+#endif
       confirm_roles(g, a);
       if (rp_of(g, P.role) & RP_ROBBED) {
         int th = holder_checked(g, 1);

@@ -1947,24 +1947,38 @@ CIT_HD int cit_carry_out(CitGame& g, const CitOpt& o, CitMT& rng) {
   switch (o.name) {
     case O_ROLE_PICK: {                                      // :6-30
       int rk = o.a;
-      P.role = g.roles[rk];
-      g.rtc &= (uint8_t)~(1u << rk);
-      uint16_t rtc_mask = (uint16_t)(g.rtc << 1);
-      uint16_t before = (uint16_t)(0x1FE & ~rtc_mask & ~(1u << (rk + 1)));
 #if CIT_WAVE
       {
-        // turn_orders_for_roles is a permutation: one lane per seat
-        int i = cit_lane();
-        int p = cit_ld(g.turn, i, i < CIT_NP, 0);
-        uint64_t at = cit_ballot(i < CIT_NP && p == a);
-        int pos_a = at ? 63 - __clzll((long long)at) : 0;   // the last match, as the loop's
-        if (i < CIT_NP && p != a) P.kr[p] = (uint16_t)((P.kr[p] & KR_CONFIRMED) | (i < pos_a ? before : rtc_mask));
-        int last = cit_readlane(p, CIT_NP - 1);
+        // turn_orders_for_roles is a permutation.  One round of loads: the
+        // role id, the roles left, the turn order (lane i) and the mover's
+        // role knowledge (lane j: seat j); seat j's place in the turn order
+        // then comes from readlanes, so the knowledge is not loaded behind it
+        const int i = cit_lane();
+        const int rid = g.roles[rk], rtc0 = g.rtc;
+        const int p = g.turn[i < CIT_NP ? i : 0], krj = P.kr[i < CIT_NP ? i : 0];
+        __asm__ volatile("" ::"v"(rid), "v"(rtc0), "v"(p), "v"(krj));
+        P.role = (uint8_t)rid;
+        const uint8_t rtc = (uint8_t)(rtc0 & ~(1u << rk));
+        g.rtc = rtc;
+        const uint16_t rtc_mask = (uint16_t)(rtc << 1);
+        const uint16_t before = (uint16_t)(0x1FE & ~rtc_mask & ~(1u << (rk + 1)));
+        const uint64_t at = cit_ballot((i < CIT_NP) & (p == a));
+        const int pos_a = at ? 63 - __clzll((long long)at) : 0;   // the last match, as the loop's
+        int ij = -1;
+#pragma unroll
+        for (int q = 0; q < CIT_NP; q++) ij = cit_readlane(p, q) == i ? q : ij;
+        if (i < CIT_NP && i != a && ij >= 0)
+          P.kr[i] = (uint16_t)((krj & KR_CONFIRMED) | (ij < pos_a ? before : rtc_mask));
+        const int last = cit_readlane(p, CIT_NP - 1);
         if (a != last) gs_set(g, 0, cit_readlane(p, pos_a + 1 < CIT_NP ? pos_a + 1 : 0));
         else setup_next_player(g, -1);
         break;
       }
 #endif
+      P.role = g.roles[rk];
+      g.rtc &= (uint8_t)~(1u << rk);
+      uint16_t rtc_mask = (uint16_t)(g.rtc << 1);
+      uint16_t before = (uint16_t)(0x1FE & ~rtc_mask & ~(1u << (rk + 1)));
       int pos_a = 0;
       for (int i = 0; i < CIT_NP; i++)
         if (g.turn[i] == a) pos_a = i;

@@ -78,6 +78,7 @@ import json
 import multiprocessing as mp
 import os
 import platform
+import shutil
 import signal
 import subprocess
 import sys
@@ -102,6 +103,88 @@ REF_PY = {"1_core": 12301, "8_procs": 83869, "unit": "carry_out transitions/s",
           "where": "survey container (BASELINE.md), not this box"}
 SQ_SET = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
           "SQ_BUSY_CYCLES", "SQ_INSTS_SMEM"]
+MLP_FLOP_PER_ROW = 2 * (418 * 512 + 512 * 256 + 256 * 128 + 128 * 6)   # ValueOnlyNN(418, 512), BN folded
+FP32_MATRIX_PEAK_TF = 157.3   # v_mfma_f32_16x16x4_f32 (MI355X_MICROARCH.md)
+MLP_ROWS = 4096               # cfr_pred's rounds mode evaluates one leaf row per suspended tree (config 4: 4096)
+MLP_KERNELS = ("k_mlp_layer", "k_mlp_head")
+LINE_MAX_BYTES = 8192         # the stdout line the driver parses (round 5's 23 KB line was not parsed)
+
+
+def _r(x, sig=4):
+    """Floats to `sig` significant digits, recursively (the compact line)."""
+    if isinstance(x, float):
+        if x != x or x in (float("inf"), float("-inf")):
+            return None
+        return float("%.*g" % (sig, x))
+    if isinstance(x, dict):
+        return {k: _r(v, sig) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_r(v, sig) for v in x]
+    return x
+
+
+def _pick(d, *keys):
+    d = d or {}
+    return {k: d.get(k) for k in keys if d.get(k) is not None}
+
+
+def compact_line(out, detail_path):
+    """The one stdout line: the contract's fields, the headline roofline and CPU
+    baseline, and per CFR leg its value, one-batch value, roofline fraction,
+    traffic over §8(d)'s bytes and CPU baseline.  Everything else (counter
+    passes, traces, notes, per-rep figures) stays in the full object written to
+    `detail_path`."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "value_one_batch", "mode", "lane_errors", "unfinished_lanes", "folded",
+            "ranks")
+    line = {k: out[k] for k in keep if k in out}
+    cfg = out.get("config") or {}
+    line["config"] = _pick(cfg, "workload", "games_per_batch", "streams", "games_in_flight", "parallelism")
+    roof = out.get("roofline") or {}
+    line["roofline"] = _pick(roof, "bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_avg_ms",
+                             "kernel_avg_ms_source", "traffic_over_alg")
+    if roof.get("issue_bound"):
+        line["roofline"]["issue_bound"] = _pick(roof["issue_bound"], "bound", "frac", "salu_per_transition",
+                                                "wait_any_frac")
+    if roof.get("timed_mode"):
+        line["roofline"]["timed_mode_ms_per_step"] = roof["timed_mode"].get("ms_per_step")
+    cpu = out.get("cpu_baseline")
+    line["cpu_baseline"] = None if cpu is None else _pick(cpu, "value", "unit", "cores", "kind", "sample", "one_core",
+                                                          "cpu_model", "error")
+    if out.get("e2e"):
+        line["e2e_transitions_per_s"] = out["e2e"].get("transitions_per_s")
+    if out.get("cfr") is not None:          # --config 3|4|5 headline
+        line["cfr"] = _cfr_compact(out["cfr"])
+    legs = out.get("cfr_configs")
+    if legs:
+        line["cfr_configs"] = {k: (_cfr_compact(v) if isinstance(v, dict) and "value" in v else
+                                   {"error": str((v or {}).get("error", v))[:160]} if isinstance(v, dict) else
+                                   str(v)[:160]) for k, v in legs.items()}
+    if out.get("mlp"):
+        line["mlp"] = _pick(out["mlp"], "kernel", "rows", "tflops", "peak", "frac", "kernel_ms", "kernel_ms_source",
+                            "error")
+    line["detail"] = detail_path
+    return _r(line)
+
+
+def _cfr_compact(c):
+    roof = c.get("roofline") or {}
+    issue = roof.get("issue") or {}
+    out = _pick(c, "value", "value_one_batch", "unit", "per_gpu")
+    out["roofline"] = _pick(roof, "bound", "frac", "kernel", "kernel_avg_ms", "kernel_launches", "kernel_ms_source")
+    if roof.get("traffic_over_alg") is not None or issue.get("traffic_over_alg") is not None:
+        out["roofline"]["traffic_over_alg"] = roof.get("traffic_over_alg", issue.get("traffic_over_alg"))
+    if issue.get("salu_per_carry_out") is not None:
+        out["roofline"]["salu_per_carry_out"] = issue["salu_per_carry_out"]
+    hn = roof.get("hbm_notional") or {}
+    if hn.get("frac") is not None:
+        out["roofline"]["hbm_notional_frac"] = hn["frac"]
+    cpu = c.get("cpu_baseline")
+    if cpu:
+        out["cpu_baseline"] = _pick(cpu, "value", "one_core", "cores", "error")
+    if c.get("rounds"):
+        out["rounds"] = _pick(c["rounds"], "value", "rounds", "trees_per_round", "seconds", "loop")
+    return out
 
 
 def _oracle_worker(args):
@@ -223,13 +306,72 @@ def _rows(pattern):
     return out
 
 
+def _run_profiled(prof_args, child, outdir, timeout_s):
+    """rocprofv3 `prof_args` over `child` (its own process group, killed on
+    timeout), output under outdir.  Returns the log's path; raises on failure."""
+    os.makedirs(outdir, exist_ok=True)
+    # (a child must not overwrite the parent's full-object file)
+    child = child + ["--full-out", os.path.join(outdir, "child_full.json")]
+    cmd = ["rocprofv3"] + prof_args + ["--output-format", "csv", "-d", outdir, "-o", "run", "--"] + child
+    env = dict(os.environ, TMPDIR="/tmp")
+    logp = os.path.join(outdir, "log.txt")
+    t0 = time.perf_counter()
+    with open(logp, "w") as log:
+        p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+        rc = None
+        while rc is None:
+            try:
+                rc = p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                el = time.perf_counter() - t0
+                if el > timeout_s:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
+                    raise RuntimeError("rocprofv3 %s timed out" % " ".join(prof_args))
+                _progress("rocprofv3 %s child running (%.0f s)" % (" ".join(prof_args)[:60], el))
+    _progress("rocprofv3 %s child done (%.0f s)" % (" ".join(prof_args)[:60], time.perf_counter() - t0))
+    if rc != 0:
+        raise RuntimeError("rocprofv3 %s exited %d" % (" ".join(prof_args), rc))
+    return logp
+
+
+def _progress(msg):
+    """A progress line on stderr (long profiler children otherwise leave a
+    run silent for minutes)."""
+    print("bench: " + msg, file=sys.stderr, flush=True)
+
+
+def _child_line(logp):
+    with open(logp) as f:
+        lines = [ln for ln in f if ln.startswith("{\"pmc_child\"")]
+    if not lines:
+        raise RuntimeError("no child line in the rocprofv3 output")
+    return json.loads(lines[-1])
+
+
+def _by_leg(per_kernel, child):
+    """{kernel: {dispatch id: value}} -> {leg key: [values of its launches]}:
+    the child runs PMC_CHILD_LEGS in order and reports each leg's launches of
+    its search kernel, so a kernel's dispatches, in dispatch order, go to those
+    legs in turn (later dispatches -- e.g. config 5's overflow retries, which
+    launch k_cfr_decide -- to none)."""
+    taken, out = {}, {}
+    for key, c, _ in PMC_CHILD_LEGS:
+        k = KERNELS[c]
+        ids = sorted(per_kernel.get(k, {}))
+        n = int(child[key]["launches"])
+        mine = ids[taken.get(k, 0):taken.get(k, 0) + n]
+        taken[k] = taken.get(k, 0) + n
+        out[key] = [per_kernel[k][i] for i in mine]
+    return out
+
+
 def _pmc_pass(counters, outdir, config=2, timeout_s=150, cfr_child=False):
     """One rocprofv3 --pmc pass over a short child run of this script (its own
     process group, killed on timeout).  Config 2: {counter: mean per launch of
     k_rollout_u}.  cfr_child: the child runs configs 3 / 4 / 5 once each
     (--pmc-child) and the result is {kernel: {counter: sum over its launches,
     "_launches": n}, "_child": the child's JSON line}.  Raises on failure."""
-    os.makedirs(outdir, exist_ok=True)
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-pmc"]
     if cfr_child:
         child += ["--pmc-child"]
@@ -237,50 +379,24 @@ def _pmc_pass(counters, outdir, config=2, timeout_s=150, cfr_child=False):
         child += ["--config", str(config), "--no-cfr"]
         child += ["--steps", "2", "--warmup", "1", "--streams", "1"] if config == 2 else [
             "--cfr-reps", "1", "--cfg5-reps", "1", "--cfr-streams", "1"]
-    cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", outdir, "-o", "run", "--"] + child
-    env = dict(os.environ, TMPDIR="/tmp")
-    logp = os.path.join(outdir, "log.txt")
-    with open(logp, "w") as log:
-        p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
-        try:
-            rc = p.wait(timeout=timeout_s)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            p.wait()
-            raise RuntimeError("rocprofv3 --pmc %s timed out" % counters)
-    if rc != 0:
-        raise RuntimeError("rocprofv3 --pmc %s exited %d" % (counters, rc))
+    logp = _run_profiled(["--pmc"] + counters, child, outdir, timeout_s)
     rows = _rows(os.path.join(outdir, "**", "*counter_collection.csv"))
     if cfr_child:
-        with open(logp) as f:
-            lines = [ln for ln in f if ln.startswith("{\"pmc_child\"")]
-        if not lines:
-            raise RuntimeError("no child line in the rocprofv3 output")
-        child = json.loads(lines[-1])
-        # the child runs PMC_CHILD_LEGS in order and reports each leg's launches
-        # of its search kernel: a kernel's dispatches, in dispatch order, go to
-        # those legs in turn (later dispatches -- e.g. config 5's overflow
-        # retries, which launch k_cfr_decide -- to none)
+        child = _child_line(logp)
         per_kernel = {}
         for r in rows:
             k = next((k for k in set(KERNELS.values()) if k in r.get("Kernel_Name", "")), None)
             if k is not None and "Dispatch_Id" in r:
                 d = per_kernel.setdefault(k, {}).setdefault(int(r["Dispatch_Id"]), {})
                 d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        taken = {k: 0 for k in per_kernel}
         out = {}
-        for key, c, _ in PMC_CHILD_LEGS:
-            k = KERNELS[c]
-            ids = sorted(per_kernel.get(k, {}))
-            n = int(child[key]["launches"])
-            mine = ids[taken.get(k, 0):taken.get(k, 0) + n]
-            taken[k] = taken.get(k, 0) + n
+        for key, launches in _by_leg(per_kernel, child).items():
             tot = {}
-            for i in mine:
-                for name, v in per_kernel[k][i].items():
+            for d in launches:
+                for name, v in d.items():
                     tot[name] = tot.get(name, 0.0) + v
             if tot:
-                tot["_launches"] = len(mine)
+                tot["_launches"] = len(launches)
                 out[key] = tot
         if not out:
             raise RuntimeError("no search-kernel rows in the rocprofv3 output")
@@ -309,19 +425,8 @@ def trace_in_run(args, timeout_s=300):
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-pmc", "--no-cfr",
              "--config", "2", "--streams", "1", "--steps", str(args.steps), "--warmup", str(args.warmup),
              "--batch", str(args.batch)]
-    cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", outdir, "-o", "run", "--"] + child
-    env = dict(os.environ, TMPDIR="/tmp")
     try:
-        with open(os.path.join(outdir, "log.txt"), "w") as log:
-            p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
-            try:
-                rc = p.wait(timeout=timeout_s)
-            except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
-                p.wait()
-                raise RuntimeError("rocprofv3 --kernel-trace timed out")
-        if rc != 0:
-            raise RuntimeError("rocprofv3 --kernel-trace exited %d" % rc)
+        _run_profiled(["--kernel-trace", "--stats"], child, outdir, timeout_s)
         paths = glob.glob(os.path.join(outdir, "**", "*kernel_stats.csv"), recursive=True)
         rows = _rows(os.path.join(outdir, "**", "*kernel_stats.csv"))
         row = next(r for r in rows if KERNELS[2] in r["Name"])
@@ -358,7 +463,7 @@ CFR_PMC_PASSES = (["FETCH_SIZE"], ["WRITE_SIZE"], SQ_SET, ["SQ_INSTS_VMEM_RD", "
 # runs at its bench size: fewer trees fit in HBM at once and would search in
 # k_cfr_decide (simulate_games without the queue), not in the queue's
 # k_cfr_train_slice.  "4@512" is config 4's per-rank shard of the 8-GPU job.
-PMC_CHILD_LEGS = (("3", 3, 1024), ("4@512", 4, 512), ("4", 4, 4096), ("5", 5, 1920))
+PMC_CHILD_LEGS = (("3", 3, 1024), ("4@512", 4, 512), ("4", 4, 4096), ("5", 5, 1920), ("5@960", 5, 960))
 
 
 def pmc_in_run_cfr():
@@ -384,7 +489,46 @@ def pmc_in_run_cfr():
     return out
 
 
-def search_roofline(pmc, alg_bytes_per_carry, timed_ms, timed_carry):
+def trace_in_run_cfr(timeout_s=300):
+    """rocprofv3 --kernel-trace --stats over one `bench.py --pmc-child` run (the
+    counter passes' own workload and seeds): per leg, its search kernel's
+    launches and their durations (the profiler's kernel begin / end), and the
+    value-net kernels of the child's MLP leg.  The CFR rooflines are priced on
+    these durations."""
+    outdir = tempfile.mkdtemp(prefix="bench_cfrtrace_", dir="/tmp")
+    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-pmc", "--pmc-child"]
+    try:
+        logp = _run_profiled(["--kernel-trace", "--stats"], child, outdir, timeout_s)
+        child_line = _child_line(logp)
+        rows = _rows(os.path.join(outdir, "**", "*kernel_trace.csv"))
+        per_kernel, mlp = {}, {}
+        for r in rows:
+            name = r.get("Kernel_Name", "")
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+            k = next((k for k in set(KERNELS.values()) if k in name), None)
+            if k is not None:
+                per_kernel.setdefault(k, {})[int(r["Dispatch_Id"])] = dur
+            m = next((m for m in MLP_KERNELS if m in name), None)
+            if m is not None:
+                mlp.setdefault(m, []).append(dur)
+        out = {}
+        for key, durs in _by_leg(per_kernel, child_line).items():
+            if durs:
+                out[key] = {"launches": len(durs), "kernel_ms_total": float(sum(durs)),
+                            "kernel_avg_ms": float(sum(durs) / len(durs)), "carry_outs": child_line[key]["carry_outs"]}
+        if mlp and child_line.get("mlp"):
+            calls = int(child_line["mlp"]["calls"])
+            out["mlp"] = {"calls": calls, "rows": child_line["mlp"]["rows"],
+                          "kernel_ms_per_call": sum(sum(v) for v in mlp.values()) / max(1, calls),
+                          "per_kernel_avg_ms": {k: sum(v) / len(v) for k, v in mlp.items()}}
+        out["_stats_csv"] = (glob.glob(os.path.join(outdir, "**", "*kernel_stats.csv"), recursive=True) or [None])[0]
+        out["_command"] = "rocprofv3 --kernel-trace --stats -- python bench.py --pmc-child --no-pmc --no-cpu-baseline"
+        return out
+    except Exception as e:  # a missing profiler must not cost the bench line
+        return {"error": str(e)[:300]}
+
+
+def search_roofline(pmc, alg_bytes_per_carry, timed_ms, timed_carry, trace=None):
     """The latency / issue model of a search kernel from its in-run counters
     (totals over the child's launches, priced per carry_out; the child runs
     the timed rep's seeds, unwarmed and serialised by the profiler, so its own
@@ -417,6 +561,16 @@ def search_roofline(pmc, alg_bytes_per_carry, timed_ms, timed_carry):
         per = 2 * 1024 * pmc["FETCH_SIZE"] / c0 + 1024 * pmc["WRITE_SIZE"] / c1
         out["traffic_bytes_per_carry_out"] = per
         out["traffic_over_alg"] = per / alg_bytes_per_carry if alg_bytes_per_carry else None
+    if trace and trace.get("kernel_ms_total"):
+        # priced on the kernel trace of the same workload (the counter child's seeds, so its carry_outs): the
+        # SALU floor of its carry_outs over the profiler's summed kernel durations
+        floor_ms = salu / carry * float(trace["carry_outs"]) / SALU_PEAK * 1e3
+        out["salu_frac_timed_search"] = out["salu_frac"]
+        out["salu_frac"] = floor_ms / trace["kernel_ms_total"]
+        out["kernel_ms_total"] = trace["kernel_ms_total"]
+        out["kernel_avg_ms"] = trace["kernel_avg_ms"]
+        out["kernel_launches"] = trace["launches"]
+        out["salu_inst_per_s"] = salu / carry * float(trace["carry_outs"]) / (trace["kernel_ms_total"] * 1e-3)
     return out
 
 
@@ -574,12 +728,17 @@ def run_rollout(args, world, rank, dev, n_dev, pmc):
                     "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_transition": 2 * L.GAME_BYTES,
                     "model": "SURVEY §8(d): 2 x CIT_GAME_BYTES per transition over the kernel time (the row stays in "
                              "LDS, so these bytes never reach HBM)"}
+    # the contract's roofline: SURVEY §8(d)'s algorithmic bytes over the kernel's own duration against HBM
+    # peak, `traffic` the counter bytes per launch; what actually binds the kernel (scalar issue and the
+    # per-wave latency chain: the row lives in LDS) is `issue_bound`
+    roof = {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": hbm_achieved / HBM_PEAK_GBS,
+            "traffic_over_alg": (traffic / alg_bytes) if traffic else None}
     if issue is not None:
-        roof = {"bound": "salu-issue", "achieved": issue["salu_inst_per_s"] / 1e9, "peak": SALU_PEAK / 1e9,
-                "unit": "G SALU inst/s", "frac": issue["salu_frac"]}
-    else:
-        roof = {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": hbm_achieved / HBM_PEAK_GBS, "note": "no SQ counters in this run: the notional HBM figure"}
+        roof["issue_bound"] = {"bound": "salu-issue", "achieved": issue["salu_inst_per_s"] / 1e9,
+                               "peak": SALU_PEAK / 1e9, "unit": "G SALU inst/s", "frac": issue["salu_frac"],
+                               "salu_per_transition": issue["salu_per_transition"],
+                               "wait_any_frac": issue.get("wait_any_frac")}
     roof.update({
         "traffic": traffic, "kernel": KERNELS[2] if args.games_per_block <= 0 else "k_rollout (lanes)",
         "kernel_avg_ms": avg_ms, "launches": K,
@@ -680,7 +839,8 @@ def _value_net(dev):
     return models.ValueNet(m, dev)
 
 
-def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, warm_rep=True, n_reps=None):
+def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, warm_rep=True, n_reps=None,
+            trace=None):
     """One of BASELINE configs 3-5 (tools/bench_selfplay.py's harness): median
     of `args.cfr_reps` timed reps after one warm-up.  `per_gpu` overrides the
     positions / trees per GPU (the per-rank shard of an 8-GPU config).  `pmc`:
@@ -753,7 +913,7 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
     if config == 3 and args.cfr_streams > 1:
         streams = _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap)
     rounds = None
-    if config == 5 and args.cfg5_rounds > 1 and warm_rep and not shard_leg:
+    if config == 5 and args.cfg5_rounds > 1 and warm_rep:
         rounds = _cfg5_rounds(args, world, rank, dev, iters, per_gpu)
     if rank != 0:
         return None
@@ -768,16 +928,20 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
                     "alg_bytes": alg, "alg_bytes_per_carry_out": alg / max(1.0, carry_all), "search_ms": ms,
                     "model": "SURVEY §8(d) CFR expand bytes: 5 x CIT_GAME_BYTES per node created + 24 B per edge "
                              "slot, over the search's wall time per GPU"}
-    issue = search_roofline(pmc, alg / max(1.0, carry_all), ms, carry_all) if pmc else None
+    issue = search_roofline(pmc, alg / max(1.0, carry_all), ms, carry_all, trace=trace) if pmc else None
     if issue is not None and issue.get("salu_frac") is not None:
         roof = {"bound": "latency (salu-issue floor)", "achieved": issue["salu_inst_per_s"] / 1e9,
                 "peak": SALU_PEAK / 1e9, "unit": "G SALU inst/s", "frac": issue["salu_frac"],
                 "traffic_bytes_per_carry_out": issue.get("traffic_bytes_per_carry_out"),
                 "traffic": issue.get("traffic_bytes_per_carry_out"),
+                "traffic_over_alg": issue.get("traffic_over_alg"),
+                "kernel_avg_ms": issue.get("kernel_avg_ms"), "kernel_launches": issue.get("kernel_launches"),
+                "kernel_ms_source": ("rocprofv3 --kernel-trace of the counter child's workload (same seeds)"
+                                     if issue.get("kernel_avg_ms") else "host wall clock of the timed search"),
                 "model": "one wave per tree runs a serial search: the SALU floor (the counter run's "
-                         "SQ_INSTS_SALU per carry_out x the timed carry_outs / (256 CU x 2.4 GHz)) over the timed "
-                         "search, with the wait fraction and VMEM instructions per carry_out; hbm_notional keeps "
-                         "SURVEY §8(d)'s bytes"}
+                         "SQ_INSTS_SALU per carry_out x the traced run's carry_outs / (256 CU x 2.4 GHz)) over "
+                         "the traced kernel time, with the wait fraction and VMEM instructions per carry_out; "
+                         "hbm_notional keeps SURVEY §8(d)'s bytes"}
     else:
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -855,48 +1019,85 @@ def _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap):
 
 
 def _cfg5_rounds(args, world, rank, dev, iters, per_gpu):
-    """Config 5 as train_from_scratch generates it, round after round:
-    `--cfg5-rounds` rounds of `per_gpu` trees per GPU through ONE
-    selfplay.TreeQueue, every round added up front, so round r + 1's trees
-    search in the slots (and arena blocks) round r's finished trees free
-    while its longest trees run on; each round's targets are all-gathered
-    when it completes.  `value` = all trees / the whole run; `steady_state` =
-    trees per round / the mean time between consecutive rounds' completions
-    (the rate once the queue is full, the first round's ramp excluded)."""
-    from citadels_self_play_amd import selfplay
+    """Config 5 as train_from_scratch generates it: train_from_scratch.collect
+    itself (its cross-round tree queue with the lookahead's admission rule --
+    round r + 1 enters once round r's first walked trees project a shortfall
+    -- and the async target all-gathers that keep a rank's slices running
+    while it waits for slower ranks) for `--cfg5-rounds` data rounds of
+    `per_gpu` trees per GPU (min_targets unbounded, so every round is needed
+    and no round past the last is started).  `value` = all trees / the whole
+    run, the first round's ramp and the last round's tail included."""
+    from types import SimpleNamespace
+    from citadels_self_play_amd import train_from_scratch as tfs
     R = args.cfg5_rounds
+    targs = SimpleNamespace(iters=iters, games_per_gpu=per_gpu, node_cap=None, seed=CFR_SEED + 90_000_000,
+                            on_error="drop", save_tuples=False, lookahead=True)
     torch.cuda.synchronize()
     _barrier(world)
     t0 = time.perf_counter()
-    q = selfplay.TreeQueue(iters, per_gpu)
-    for r in range(R):
-        q.add(selfplay.shard(per_gpu * world, base_seed=CFR_SEED + (90 + r) * 1_000_000))
-    n_targets, errs, carry = 0, 0, 0.0
-    for r in range(R):
-        q.run(r)
-        _, stats, t = q.result(r)
-        f, v = selfplay.all_gather_targets(t["feat"], t["value"])
-        n_targets += int(f.shape[0])
-        errs += int((stats[:, 4] != 0).sum())
-        carry += float(stats[:, 3].double().sum())
-    done = [q.rounds[r].t_done - t0 for r in range(R)]
-    S, oc = q.S, q.overcommit
-    q.close()
+    feat, value, _ = tfs.collect(rank, world, targs, 0, 10 ** 15, lambda m: None, max_rounds=R)
     torch.cuda.synchronize()
     _barrier(world)
     el = time.perf_counter() - t0
-    el, trees, carry, errs, *done = _reduce([el, per_gpu * world * R, carry, errs] + done, world, dev,
-                                            maxes=tuple(range(0, 1)) + tuple(range(4, 4 + R)))
-    gaps = np.diff(done)
+    done = [t - t0 for t in tfs.collect.round_done]
+    dropped = sum(tfs.collect.dropped.values())
+    el, trees, dropped, *done = _reduce([el, per_gpu * world * R, dropped] + done, world, dev,
+                                        maxes=(0,) + tuple(range(3, 3 + R)))
     return {"value": trees / el, "unit": "trees/s", "rounds": R, "trees_per_round": per_gpu * world,
-            "seconds": el, "round_done_s": done,
-            "after_first_round": per_gpu * world * (R - 1) / float(done[-1] - done[0]) if R > 1 else None,
-            "first_round_s": done[0], "carry_out_per_s": carry / el, "error_lanes": int(errs),
-            "pooled_targets": n_targets, "slots": S, "overcommit": oc,
-            "note": "rounds of trees through one TreeQueue, all added up front (the next round's trees take the "
-                    "slots the current round's tail frees); value = all trees / the whole run (first round's ramp "
-                    "and last round's tail included); after_first_round = the later rounds' trees / the time "
-                    "between the first and the last round's completion (they started earlier: an upper figure)"}
+            "seconds": el, "round_done_s": done, "first_round_s": done[0],
+            "dropped_trees": int(dropped), "pooled_targets": int(feat.shape[0]),
+            "loop": "train_from_scratch.collect (lookahead admission, async all-gathers)",
+            "note": "value = all rounds' trees / the whole run; one round alone is value_one_batch"}
+
+
+def _mlp_rows(dev, rows):
+    """encode_game rows of `rows` config-4 positions (the rows cfr_pred's rounds
+    mode hands the value net: one leaf per suspended tree)."""
+    from citadels_self_play_amd import _lib, selfplay
+    from citadels_self_play_amd.engine import GameBatch
+    b = GameBatch(selfplay.shard(rows, base_seed=CFR_SEED + 7_000_000), preset=True, device=dev)
+    b.advance_random(0, 300)
+    feat = torch.zeros((rows, 418), dtype=torch.float32, device=dev)
+    _lib.check(b.lib.cit_encode_games(b.games.data_ptr(), rows, -1, feat.data_ptr(),
+                                      torch.cuda.current_stream(dev).cuda_stream), "cit_encode_games")
+    return feat
+
+
+def run_mlp(dev, calls=20, warm=3, rows=MLP_ROWS, trace=None):
+    """The value net's MFMA forward (ValueNet.forward: k_mlp_layer x 2 +
+    k_mlp_head, v_mfma_f32_16x16x4_f32) on `rows` encode_game rows, as
+    cfr_pred's rounds mode calls it: HIP events around each call on the
+    stream it runs on; TF/s = MLP_FLOP_PER_ROW x rows / time against the fp32
+    matrix peak.  `trace`: the kernel trace's per-call kernel time (summed
+    durations of the three kernels, launch gaps excluded)."""
+    net = _value_net(dev)
+    feat = _mlp_rows(dev, rows)
+    for _ in range(warm):
+        net.forward(feat)
+    st = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(calls)]
+    torch.cuda.synchronize()
+    for a, b in evs:
+        a.record(st)
+        net.forward(feat)
+        b.record(st)
+    torch.cuda.synchronize()
+    ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    flop = MLP_FLOP_PER_ROW * rows
+    out = {"kernel": "+".join(MLP_KERNELS) + " (ValueNet.forward, fp32 MFMA 16x16x4)", "rows": rows,
+           "flop_per_row": MLP_FLOP_PER_ROW, "call_ms_events": ms, "calls": calls,
+           "tflops_events": flop / (ms * 1e-3) / 1e12, "peak": FP32_MATRIX_PEAK_TF, "unit": "TFLOP/s",
+           "path": "cfr_pred rounds mode's leaf batch (engine.GameBatch._cfr_pred: one row per suspended tree); "
+                   "config 4's timed path evaluates leaves inside the search kernel instead (cit_mlp_wave.h)"}
+    km = (trace or {}).get("kernel_ms_per_call")
+    out["kernel_ms"] = km if km else ms
+    out["kernel_ms_source"] = ("rocprofv3 --kernel-trace (summed kernel durations per call, in-run child)" if km
+                               else "HIP events around each call")
+    out["tflops"] = flop / (out["kernel_ms"] * 1e-3) / 1e12
+    out["frac"] = out["tflops"] / FP32_MATRIX_PEAK_TF
+    if trace:
+        out["trace"] = trace
+    return out
 
 
 def _cpu_model():
@@ -937,6 +1138,9 @@ def main():
     ap.add_argument("--cfg5-iters", type=int, default=200000, help="config 5 cfr_train iterations per tree")
     ap.add_argument("--cfg5-rounds", type=int, default=3,
                     help="config 5: data rounds through one cross-round tree queue (the `rounds` figure; 1 = off)")
+    ap.add_argument("--no-mlp", action="store_true", help="skip the value-net MFMA figure (`mlp`)")
+    ap.add_argument("--full-out", default="gpurun_out/bench/bench_full.json",
+                    help="the full bench object (the stdout line is its compact summary)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the real path); gloo only to rehearse N>1 ranks on one GPU")
     args = ap.parse_args()
@@ -965,6 +1169,9 @@ def main():
             m = r["median"]
             line[key] = {"carry_outs": m["carry_out_per_s"] * m["seconds"], "search_ms": m["seconds"] * 1e3,
                          "launches": engine.LAUNCHES.get(KERNELS[c], 0) - before}
+        if not args.no_mlp:
+            m = run_mlp(dev, calls=10, warm=2)
+            line["mlp"] = {"calls": 12, "rows": m["rows"]}
         print(json.dumps(line), flush=True)
         return
 
@@ -973,6 +1180,7 @@ def main():
     if pmc is not None:
         pmc["trace"] = trace_in_run(args)
     cfr_pmc = pmc_in_run_cfr() if (world == 1 and not args.no_pmc and (cfr_list or args.config != 2)) else {}
+    cfr_trace = trace_in_run_cfr() if (world == 1 and not args.no_pmc and (cfr_list or args.config != 2)) else {}
 
     dev = torch.device("cuda", local % max(1, n_dev))
     if world > 1:
@@ -982,8 +1190,11 @@ def main():
 
     if args.config == 2:
         out = run_rollout(args, world, rank, dev, n_dev, pmc)
+        if rank == 0:
+            _progress("config 2 done: %.4g carry_out/s" % out["value"])
     else:
-        c = run_cfr(args.config, args, world, rank, dev, pmc=cfr_pmc.get(str(args.config)))
+        c = run_cfr(args.config, args, world, rank, dev, pmc=cfr_pmc.get(str(args.config)),
+                    trace=cfr_trace.get(str(args.config)))
         out = None
         if rank == 0:
             out = {"metric": "MCCFR config %d" % args.config, "value": c["value"], "unit": c["unit"],
@@ -1003,15 +1214,25 @@ def main():
             c, _, n = key.partition("@")
             c = int(c)
             r = run_cfr(c, args, world, rank, dev, pmc=cfr_pmc.get(key), per_gpu=int(n) if n else None,
-                        cpu=not n)
+                        cpu=not n, trace=cfr_trace.get(key))
             if n and r is not None:
                 r["shard_of"] = {4: "config 4's 4096 positions over 8 GPUs (the per-rank work of that config)",
-                                 5: "config 5 / train_from_scratch at its default --games-per-gpu"}.get(c)
+                                 5: "config 5 / train_from_scratch at half its default --games-per-gpu"}.get(c)
             cfr_out[key] = r
+            if rank == 0:
+                _progress("cfr leg %s done: %.4g %s" % (key, r["value"], r["unit"]))
         except Exception as e:          # a CFR leg must not cost the headline line
             cfr_out[key] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
     if cfr_pmc.get("error") and rank == 0:
         cfr_out["pmc_error"] = cfr_pmc["error"]
+    if cfr_trace.get("error") and rank == 0:
+        cfr_out["trace_error"] = cfr_trace["error"]
+    mlp = None
+    if args.config == 2 and not args.no_mlp and cfr_list:
+        try:
+            mlp = run_mlp(dev, trace=cfr_trace.get("mlp"))
+        except Exception as e:          # nor the value-net figure
+            mlp = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
 
     if rank == 0:
         if folded:
@@ -1024,7 +1245,31 @@ def main():
                 out["cpu_baseline"] = None
         if cfr_list:
             out["cfr_configs"] = cfr_out
-        print(json.dumps(out), flush=True)
+        if mlp is not None:
+            out["mlp"] = mlp
+        if cfr_trace:
+            out["cfr_trace"] = cfr_trace
+        # the full object (counter passes, traces, notes) goes to a file beside the profiler CSVs; stdout
+        # gets one compact line (< LINE_MAX_BYTES) naming it
+        full = os.path.join(ROOT, args.full_out) if not os.path.isabs(args.full_out) else args.full_out
+        detail = os.path.relpath(full, ROOT) if full.startswith(ROOT) else full
+        try:
+            os.makedirs(os.path.dirname(full), exist_ok=True)
+            for src, name in (((pmc or {}).get("trace") or {}).get("stats_csv"), "rollout_kernel_stats.csv"), (
+                    cfr_trace.get("_stats_csv"), "cfr_kernel_stats.csv"):
+                if src and os.path.exists(src):
+                    shutil.copy(src, os.path.join(os.path.dirname(full), name))
+            with open(full, "w") as f:
+                json.dump(out, f, indent=1)
+        except OSError as e:
+            detail = "not written: %s" % e
+        line = compact_line(out, detail)
+        txt = json.dumps(line)
+        if len(txt) > LINE_MAX_BYTES:        # never again an unparseable line: drop the CFR legs' detail first
+            line["cfr_configs"] = {k: _pick(v, "value", "value_one_batch", "unit") if isinstance(v, dict) else v
+                                   for k, v in (line.get("cfr_configs") or {}).items()}
+            txt = json.dumps(line)
+        print(txt, flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -21,7 +21,6 @@ _SIGS = {
     "cit_game_bytes": ([], i32),
     "cit_seer_scratch_words": ([], i32),
     "cit_layout": ([vp, i32], i32),
-    "cit_area_test": ([vp, vp, vp, i32, vp, i32, vp, vp], i32),
     "cit_mt_seed": ([vp, vp, i32, vp, i32, vp], i32),
     "cit_mt_draw": ([vp, vp, i32, i32, vp, vp], i32),
     "cit_init": ([vp, vp, vp, i32, vp, i32, vp], i32),

@@ -72,6 +72,13 @@ __device__ __forceinline__ uint64_t cit_wave_or64(uint64_t v) {
 #ifndef CIT_BUILD_CAP
 #define CIT_BUILD_CAP 16
 #endif
+// the wave paths load a player's buildings one per lane with the lane index
+// masked by CIT_BUILD_CAP - 1 (cit_engine.h: do_finish, gold_or_card, ...)
+static_assert(CIT_BUILD_CAP > 0 && (CIT_BUILD_CAP & (CIT_BUILD_CAP - 1)) == 0 && CIT_BUILD_CAP <= 64,
+              "CIT_BUILD_CAP: a power of two of at most 64");
+// roles with a role_properties entry (game.py:525-534: rank ids 0..7); the
+// rank-8 roles 24..26 and the Bewitched (>= 27) are KeyErrors there
+#define CIT_RP_ROLES 24
 #define CIT_DECK_CAP 128          // ring buffer, power of two
 #define CIT_DISCARD_CAP 88        // >= the 76 cards a game deals
 #define CIT_USED_CAP 80
@@ -424,6 +431,32 @@ __device__ __attribute__((noinline)) void mt_twist_coop(cit_lds_u32* m) {
     }
   }
 }
+// The same twist inline, for a unit whose search functions are out of line
+// (cit_cfr.hip): a call to mt_twist_coop makes its caller a non-leaf function,
+// which must save its return address through a callee-saved VGPR spilled to
+// scratch and reload it before returning (a scratch round trip on every call of
+// eng_carry, eng_prepare, eng_sample, cfr_choose, ...), for a twist that runs
+// once per 624 draws.  One wave owns the stream, so ten 64-word chunks in
+// order need no barrier (LDS operations of one wave are in order): in chunk c
+// word i reads old words i and i + 1 (or the new word 0 for i = 623) and word
+// (i + 397) mod 624, which is old for i < 227 (a later chunk) and new for
+// i >= 227 (i - 227 lies in an earlier chunk) -- the serial recurrence.
+__device__ __forceinline__ void mt_twist_wave(cit_lds_u32* m) {
+  const int ln = (int)__lane_id();
+#pragma unroll 1
+  for (int c = 0; c < CIT_MT_N; c += 64) {
+    const int i = c + ln;
+    const int ic = i < CIT_MT_N ? i : 0;
+    const int i1 = ic + 1 < CIT_MT_N ? ic + 1 : 0;
+    const int k = ic + 397 < CIT_MT_N ? ic + 397 : ic + 397 - CIT_MT_N;
+    const uint32_t y = (m[ic] & 0x80000000u) | (m[i1] & 0x7fffffffu);
+    const uint32_t v = m[k] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    if (i < CIT_MT_N) m[i] = v;
+  }
+}
+#ifndef CIT_TWIST_INLINE
+#define CIT_TWIST_INLINE 1
+#endif
 #endif
 
 CIT_HD uint32_t mt_temper(uint32_t y) {
@@ -438,7 +471,11 @@ CIT_HD uint32_t mt_next(CitMT& r) {
   uint32_t i = r.pos;
   if (i >= CIT_MT_N) {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(CIT_MT_COOP_ONLY)
-    mt_twist_coop((cit_lds_u32*)r.mt);   // a unit whose every stream is an LDS coop stream
+    // a unit whose every stream is an LDS coop stream
+    if (CIT_TWIST_INLINE)
+      mt_twist_wave((cit_lds_u32*)r.mt);
+    else
+      mt_twist_coop((cit_lds_u32*)r.mt);
     r.win_base = -1;
 #elif defined(__HIP_DEVICE_COMPILE__)
     if (r.coop) {

@@ -19,7 +19,6 @@
 #endif
 
 #include "../../include/citadels.h"
-#include "cit_area_test.h"
 #include "cit_engine.h"
 #include "cit_lanes.h"
 
@@ -453,20 +452,6 @@ __global__ __launch_bounds__(64) void k_close_position(uint32_t* games, uint32_t
   });
 }
 
-// cit_area_test.h's operation sequence on each lane's game (the wave paths of
-// the card-area list operations; the host build runs the scalar ones).
-__global__ __launch_bounds__(64) void k_area_test(uint32_t* games, uint32_t* mt, uint32_t* idx, int B,
-                                                 const uint64_t* seeds, int n_ops, uint32_t* log) {
-  uniform_game<false, true>(games, mt, idx, B, [&](CitGame& g, CitMT& r, long l) {
-    uint64_t s = seeds[l] | 1ull;
-    for (int i = 0; i < n_ops && !g.err; i++) {
-      uint32_t v = 0;
-      area_test_op(g, r, s, &v);
-      if (threadIdx.x == 0) log[l * n_ops + i] = v;
-    }
-  });
-}
-
 }  // namespace
 
 #define CHECK_LAUNCH()                       \
@@ -503,7 +488,7 @@ int cit_roll_clock_read(unsigned long long* out, int n) {
 }
 #endif
 
-int cit_abi_version(void) { return 8; }
+int cit_abi_version(void) { return 9; }
 int cit_game_bytes(void) { return CIT_GAME_BYTES; }
 int cit_seer_scratch_words(void) { return CIT_SEER_MAX; }
 
@@ -650,13 +635,6 @@ int cit_advance_policy(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t* se
   if (B <= 0 || !games || !mt || !mt_idx || !seer || !status || !steps) return -1;
   hipLaunchKernelGGL(k_advance_policy, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt,
                      mt_idx, seer, B, search_mask, max_steps < 0 ? CIT_ROLLOUT_CAP : max_steps, status, steps);
-  CHECK_LAUNCH();
-}
-
-int cit_area_test(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int n_ops, uint32_t* log,
-                  hipStream_t stream) {
-  if (B <= 0 || n_ops < 0 || !games || !mt || !mt_idx || !seeds || (n_ops && !log)) return -1;
-  hipLaunchKernelGGL(k_area_test, dim3(B), dim3(64), 0, stream, (uint32_t*)games, mt, mt_idx, B, seeds, n_ops, log);
   CHECK_LAUNCH();
 }
 

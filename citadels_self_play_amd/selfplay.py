@@ -488,118 +488,133 @@ class TreeQueue:
     def run(self, r=None, on_slice=None):
         """Slices until round r (default: every round added) is complete;
         on_slice(queue) after each slice (may add rounds)."""
-        from .engine import ERR_OVERFLOW, ERR_POOL, ERR_POOL_ARENA
-        sb, state, dev, S = self.sb, self.state, self.dev, self.S
-        tq = time.perf_counter()
         while True:
             self._stamp()
             if r is not None and self.done(r):
                 break
-            self.running.zero_()
-            paused = None
-            if self.planner is not None:
-                st_np = state.cpu().numpy()
-                live = (self.slot_q.cpu().numpy() >= 0) & (st_np[:, 6] != CP_DONE)
-                pmask = self.planner.plan(st_np, live, self.ran)
-                self.ran = live & ~pmask
-                if pmask.any():
-                    paused = torch.from_numpy(np.flatnonzero(pmask)).to(dev)
-                    saved = state[paused, 6].clone()
-                    state[paused, 6] = CP_DONE           # sits this slice out (the kernel returns at once)
-            tq = self._tick("plan", tq)
-            sb.train_slice(self.iters, state, self.ticks, self.chosen, self.stats, self.running)
-            self.n_slices += 1
-            if self.pending is not None:
-                # last slice's finished trees: their targets are walked on a second stream while this
-                # slice runs (their slots sit this slice out, their blocks stay held until the walk ends)
-                p_slots, p_qs = self.pending
-                with torch.cuda.stream(self.side):      # (everything it reads was complete at the last sync)
-                    roots = torch.full((S,), -1, dtype=torch.int32, device=dev)
-                    for R, loc, sl in self._split(p_qs, p_slots):
-                        roots[sl] = _roots_for_targets(R.out_stats[loc])
-                    t = sb._cfr_targets(roots, 0)
-                    for R, loc, sl in self._split(p_qs, p_slots):
-                        R.parts.append((t, sl, loc))
-            # the slice and the walk -- not the device: an overflowed tree searched again on the
-            # retry stream (seconds for a 200k tree) must not hold the queue's next slice
-            torch.cuda.current_stream(dev).synchronize()
-            self.side.synchronize()
-            tq = self._tick("slice+targets", tq)
-            if paused is not None:
-                state[paused, 6] = saved
-                self.running += int(paused.numel())       # paused trees are unfinished
-            free = []
-            if self.pending is not None:
-                p_slots, p_qs = self.pending
-                for R, loc, sl in self._split(p_qs, p_slots):
-                    R.src.scatter(sb.subset(sl), loc)
-                sb.release(p_slots)
-                free.append(p_slots)
-                self.pending = None
-            done = ((state[:, 6] == CP_DONE) & (self.slot_q >= 0)).nonzero().flatten()
-            if done.numel():
-                qs = self.slot_q[done]
-                st_done = self.stats[done]
-                # max_requeue > 0: a tree stopped only by the shared arena running out starts again
-                # from its position later in the queue (the same search, bit for bit; at most
-                # max_requeue times, then the final retry)
-                redo = torch.zeros(done.numel(), dtype=torch.bool, device=dev)
-                (n_used, e_used), (n_cap, e_cap) = sb.arena_used() if self.max_requeue else ((0, 0), (1, 1))
-                if n_used > n_cap or e_used > e_cap:
-                    st_np = st_done.cpu().numpy()
-                    for i, (q, row) in enumerate(zip(qs.cpu().tolist(), st_np)):
-                        if row[4] == ERR_OVERFLOW | ERR_POOL_ARENA and self.retries.get(q, 0) < self.max_requeue:
-                            self.retries[q] = self.retries.get(q, 0) + 1
-                            redo[i] = True
-                            self.requeue.append(q)
-                            self.n_requeued += 1
-                fin = ~redo
-                ov = fin & ((st_done[:, 4] & ERR_POOL) != 0)        # pool overflows: searched again
-                if bool(ov.any()):
-                    for R, loc, sl in self._split(qs[ov]):
-                        R.early.append(_early_retry(R.snap, loc, st_done[ov][(qs[ov] >= R.base) &
-                                                                             (qs[ov] < R.base + R.Q)],
-                                                    self.iters, self.node_cap, self.edge_cap, self.rstream))
-                    if self.log is not None:
-                        self.log("simulate_queue: tree(s) %s overflowed after slice %d (nodes, edges: %s of caps %d, "
-                                 "%d); searched again beside the queue"
-                                 % (qs[ov].tolist(), self.n_slices, st_done[ov][:, 1:3].tolist(), self.node_cap,
-                                    self.edge_cap))
-                if bool(fin.any()):
-                    qf, sf = qs[fin], st_done[fin]
-                    cf = self.chosen[done[fin]]
-                    for R in self.rounds:
-                        m = (qf >= R.base) & (qf < R.base + R.Q)
-                        if bool(m.any()):
-                            R.out_stats[qf[m] - R.base] = sf[m]
-                            R.out_chosen[qf[m] - R.base] = cf[m]
-                            R.n_done += int(m.sum())
-                    self.pending = (done[fin], qf)
-                    self.slot_q[done[fin]] = -2                 # held: targets pending
-                if bool(redo.any()):
-                    sb.release(done[redo])
-                    free.append(done[redo])
-                    self.slot_q[done[redo]] = -1
-                if self.log is not None:
-                    self.log("simulate_queue: %s trees done after %d slices"
-                             % (" + ".join("%d of %d" % (R.n_done, R.Q) for R in self.rounds), self.n_slices))
-            if free:
-                self._fill(torch.cat(free))
-            if on_slice is not None:
-                on_slice(self)
-            tq = self._tick("finish", tq)
-            if self.qtrace is not None:
-                held = self.planner.held().sum(0).tolist() if self.planner is not None else None
-                self.qtrace.write(json.dumps({
-                    "slice": self.n_slices, "t": round(time.perf_counter() - self.t_q0, 4),
-                    "slots_busy": int((self.slot_q >= 0).sum()), "searching": int(self.ran.sum()),
-                    "paused": 0 if paused is None else int(paused.numel()),
-                    "done": [R.n_done for R in self.rounds], "held_blocks": held,
-                    "arena_blocks": None if self.planner is None else self.planner.cap.tolist()}) + "\n")
-            if (int(self.running.item()) == 0 and self.pending is None and bool((self.slot_q < 0).all())
-                    and not self.requeue):
+            if not self.step(on_slice):
                 break
         self._stamp()
+
+    def idle(self):
+        """True when no tree is searching, waiting for its target walk or queued."""
+        return (self.pending is None and bool((self.slot_q < 0).all()) and not self.requeue
+                and self.nxt >= self.total)
+
+    def step(self, on_slice=None):
+        """One slice of every searching tree (the finished trees of the last
+        slice walked beside it, freed slots refilled).  Returns False once the
+        queue has nothing left to search."""
+        from .engine import ERR_OVERFLOW, ERR_POOL, ERR_POOL_ARENA
+        sb, state, dev, S = self.sb, self.state, self.dev, self.S
+        if sb is None:
+            return False
+        tq = time.perf_counter()
+        self.running.zero_()
+        paused = None
+        if self.planner is not None:
+            st_np = state.cpu().numpy()
+            live = (self.slot_q.cpu().numpy() >= 0) & (st_np[:, 6] != CP_DONE)
+            pmask = self.planner.plan(st_np, live, self.ran)
+            self.ran = live & ~pmask
+            if pmask.any():
+                paused = torch.from_numpy(np.flatnonzero(pmask)).to(dev)
+                saved = state[paused, 6].clone()
+                state[paused, 6] = CP_DONE           # sits this slice out (the kernel returns at once)
+        tq = self._tick("plan", tq)
+        sb.train_slice(self.iters, state, self.ticks, self.chosen, self.stats, self.running)
+        self.n_slices += 1
+        if self.pending is not None:
+            # last slice's finished trees: their targets are walked on a second stream while this
+            # slice runs (their slots sit this slice out, their blocks stay held until the walk ends)
+            p_slots, p_qs = self.pending
+            with torch.cuda.stream(self.side):      # (everything it reads was complete at the last sync)
+                roots = torch.full((S,), -1, dtype=torch.int32, device=dev)
+                for R, loc, sl in self._split(p_qs, p_slots):
+                    roots[sl] = _roots_for_targets(R.out_stats[loc])
+                t = sb._cfr_targets(roots, 0)
+                for R, loc, sl in self._split(p_qs, p_slots):
+                    R.parts.append((t, sl, loc))
+        # the slice and the walk -- not the device: an overflowed tree searched again on the
+        # retry stream (seconds for a 200k tree) must not hold the queue's next slice
+        torch.cuda.current_stream(dev).synchronize()
+        self.side.synchronize()
+        tq = self._tick("slice+targets", tq)
+        if paused is not None:
+            state[paused, 6] = saved
+            self.running += int(paused.numel())       # paused trees are unfinished
+        free = []
+        if self.pending is not None:
+            p_slots, p_qs = self.pending
+            for R, loc, sl in self._split(p_qs, p_slots):
+                R.src.scatter(sb.subset(sl), loc)
+            sb.release(p_slots)
+            free.append(p_slots)
+            self.pending = None
+        done = ((state[:, 6] == CP_DONE) & (self.slot_q >= 0)).nonzero().flatten()
+        if done.numel():
+            qs = self.slot_q[done]
+            st_done = self.stats[done]
+            # max_requeue > 0: a tree stopped only by the shared arena running out starts again
+            # from its position later in the queue (the same search, bit for bit; at most
+            # max_requeue times, then the final retry)
+            redo = torch.zeros(done.numel(), dtype=torch.bool, device=dev)
+            (n_used, e_used), (n_cap, e_cap) = sb.arena_used() if self.max_requeue else ((0, 0), (1, 1))
+            if n_used > n_cap or e_used > e_cap:
+                st_np = st_done.cpu().numpy()
+                for i, (q, row) in enumerate(zip(qs.cpu().tolist(), st_np)):
+                    if row[4] == ERR_OVERFLOW | ERR_POOL_ARENA and self.retries.get(q, 0) < self.max_requeue:
+                        self.retries[q] = self.retries.get(q, 0) + 1
+                        redo[i] = True
+                        self.requeue.append(q)
+                        self.n_requeued += 1
+            fin = ~redo
+            ov = fin & ((st_done[:, 4] & ERR_POOL) != 0)        # pool overflows: searched again
+            if bool(ov.any()):
+                for R, loc, sl in self._split(qs[ov]):
+                    R.early.append(_early_retry(R.snap, loc, st_done[ov][(qs[ov] >= R.base) &
+                                                                         (qs[ov] < R.base + R.Q)],
+                                                self.iters, self.node_cap, self.edge_cap, self.rstream))
+                if self.log is not None:
+                    self.log("simulate_queue: tree(s) %s overflowed after slice %d (nodes, edges: %s of caps %d, "
+                             "%d); searched again beside the queue"
+                             % (qs[ov].tolist(), self.n_slices, st_done[ov][:, 1:3].tolist(), self.node_cap,
+                                self.edge_cap))
+            if bool(fin.any()):
+                qf, sf = qs[fin], st_done[fin]
+                cf = self.chosen[done[fin]]
+                for R in self.rounds:
+                    m = (qf >= R.base) & (qf < R.base + R.Q)
+                    if bool(m.any()):
+                        R.out_stats[qf[m] - R.base] = sf[m]
+                        R.out_chosen[qf[m] - R.base] = cf[m]
+                        R.n_done += int(m.sum())
+                self.pending = (done[fin], qf)
+                self.slot_q[done[fin]] = -2                 # held: targets pending
+            if bool(redo.any()):
+                sb.release(done[redo])
+                free.append(done[redo])
+                self.slot_q[done[redo]] = -1
+            if self.log is not None:
+                self.log("simulate_queue: %s trees done after %d slices"
+                         % (" + ".join("%d of %d" % (R.n_done, R.Q) for R in self.rounds), self.n_slices))
+        if free:
+            self._fill(torch.cat(free))
+        if on_slice is not None:
+            on_slice(self)
+        tq = self._tick("finish", tq)
+        if self.qtrace is not None:
+            held = self.planner.held().sum(0).tolist() if self.planner is not None else None
+            self.qtrace.write(json.dumps({
+                "slice": self.n_slices, "t": round(time.perf_counter() - self.t_q0, 4),
+                "slots_busy": int((self.slot_q >= 0).sum()), "searching": int(self.ran.sum()),
+                "paused": 0 if paused is None else int(paused.numel()),
+                "done": [R.n_done for R in self.rounds], "held_blocks": held,
+                "arena_blocks": None if self.planner is None else self.planner.cap.tolist()}) + "\n")
+        if (int(self.running.item()) == 0 and self.pending is None and bool((self.slot_q < 0).all())
+                and not self.requeue):
+            return False
+        return True
 
     def _stamp(self):
         for R in self.rounds:
@@ -699,7 +714,7 @@ def _overflowed(stats):
     return (stats[:, 4] & ERR_OVERFLOW) != 0
 
 
-ERROR_CLASSES = ("value_error", "terminal", "capacity", "pool")
+ERROR_CLASSES = ("value_error", "terminal", "capacity", "pool", "unsupported")
 ERR_UNSUPPORTED = 0x40       # CIT_ERR_UNSUPPORTED (csrc/cit_core.h): an engine limit, not a reference exception
 
 
@@ -711,13 +726,16 @@ def error_classes(stats, terminal):
                    ValueError from np.random.choice over an empty or NaN row,
                    ...);
       terminal     the position was already over (run_mccfr raises on it);
-      capacity     an engine limit the reference does not have: a list
-                   overflowed (CIT_ERR_OVERFLOW without a pool bit: a player
-                   holding more than 88 cards, or more than 32 hand-knowledge
-                   entries), or a branch the engine stops on
-                   (CIT_ERR_UNSUPPORTED: the magician / cardinal option tables
-                   of a hand over 32 cards);
-      pool         a node pool still overflowed after its retries."""
+      capacity     an engine list limit the reference does not have
+                   (CIT_ERR_OVERFLOW without a pool bit: a player holding more
+                   than 88 cards, or more than 32 hand-knowledge entries);
+      pool         a node pool still overflowed after its retries;
+      unsupported  CIT_ERR_UNSUPPORTED: a branch the engine stops on (the
+                   magician / cardinal option tables of a hand over 32 cards)
+                   or an engine / configuration fault (a failed tree setup,
+                   cfr_pred on a pool reset without pred, no crown holder in
+                   setup_round) -- counted apart from the list limits so a
+                   fault is never filed as an expected capacity stop."""
     from .engine import ERR_OVERFLOW, ERR_POOL
     err = stats[:, 4].cpu()
     term = terminal.cpu().to(torch.bool)
@@ -727,8 +745,9 @@ def error_classes(stats, terminal):
     cls = torch.full(err.shape, -1, dtype=torch.int64)
     cls[(err != 0) & ~over & ~unsup] = 0
     cls[term] = 1
-    cls[((over & ~pool) | (unsup & ~over)) & ~term] = 2
+    cls[over & ~pool & ~term] = 2
     cls[pool & ~term] = 3
+    cls[unsup & ~over & ~term] = 4
     return cls, {k: int((cls == i).sum()) for i, k in enumerate(ERROR_CLASSES)}
 
 
@@ -835,25 +854,39 @@ def unpack_targets(rows):
     return f, v
 
 
-def all_gather_targets(feat, value, group=None):
+def wait_driving(work, drive=None):
+    """Wait for an async collective; while it is incomplete, call drive() (e.g.
+    one slice of a tree queue) instead of blocking the host, until drive()
+    returns False (nothing left to run) -- then block."""
+    if work is None:
+        return
+    while drive is not None and not work.is_completed():
+        if not drive():
+            break
+    work.wait()
+
+
+def all_gather_targets(feat, value, group=None, drive=None):
     """Pool every rank's (encode_game, node_value) target pairs on every rank,
     in rank order: all_gather of the int64 counts, then of the rows padded to
     the largest count.  Works on any backend (RCCL on device tensors, gloo on
-    CPU tensors)."""
+    CPU tensors).  Both collectives are issued async: with `drive`, the host
+    keeps calling drive() (train_from_scratch: the next round's queue slices)
+    while a slower rank has not yet joined, instead of blocking on the counts."""
     if not (dist.is_available() and dist.is_initialized()):
         return feat, value
     ws = dist.get_world_size(group)
     dev = feat.device
     n = torch.tensor([feat.shape[0]], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(n) for _ in range(ws)]
-    dist.all_gather(counts, n, group=group)
+    wait_driving(dist.all_gather(counts, n, group=group, async_op=True), drive)
     counts = [int(c.item()) for c in counts]
     m = max(counts)
     rows = torch.zeros((m, TARGET_ROW_BYTES), dtype=torch.uint8, device=dev)
     if feat.shape[0]:
         rows[:feat.shape[0]] = pack_targets(feat, value)
     bufs = [torch.empty_like(rows) for _ in range(ws)]
-    dist.all_gather(bufs, rows, group=group)
+    wait_driving(dist.all_gather(bufs, rows, group=group, async_op=True), drive)
     pooled = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
     return unpack_targets(pooled)
 

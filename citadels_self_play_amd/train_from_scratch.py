@@ -50,7 +50,7 @@ class TreeError(ValueError):
 
 class EngineCapacityError(RuntimeError):
     """--on-error raise: a tree hit a limit of this engine that the reference
-    does not have (selfplay.error_classes "capacity" / "pool"), so its targets
+    does not have (selfplay.error_classes "capacity" / "pool" / "unsupported"), so its targets
     cannot be reproduced; not a reference exception."""
 
 
@@ -60,7 +60,7 @@ def lane_errors(stats, t, seeds):
     from .selfplay import error_classes
     cls, counts = error_classes(stats, t["terminal"])
     ref = ((cls == 0) | (cls == 1)).nonzero().flatten()
-    eng = ((cls == 2) | (cls == 3)).nonzero().flatten()
+    eng = (cls >= 2).nonzero().flatten()
     first_ref = int(seeds[int(ref[0])]) if ref.numel() else None
     first_eng = int(seeds[int(eng[0])]) if eng.numel() else None
     return counts, first_ref, first_eng
@@ -72,6 +72,12 @@ def round_seeds(args, world, phase, rnd):
     return selfplay.shard(args.games_per_gpu * world, base_seed=base)
 
 
+# _Lookahead estimates a round's targets from its first walked trees once this
+# fraction of the round is walked (round 5 waited for half, leaving the slots of
+# the earliest finished trees idle until then)
+LOOKAHEAD_WALKED = 1.0 / 8
+
+
 class _Lookahead:
     """collect's cross-round queue (selfplay.TreeQueue): while round r's
     longest trees finish, round r + 1's trees already search in the slots the
@@ -80,79 +86,118 @@ class _Lookahead:
     (the estimate only decides whether to start the next round early: the
     rounds actually used are decided by the pooled count, as in the
     reference, and a round started but not needed is dropped).  Each round's
-    trees and targets are those of simulate_games on its seeds, bit for bit."""
+    trees and targets are those of simulate_games on its seeds, bit for bit.
+    `max_rounds` (the bench's fixed-round runs) never starts a round past it."""
 
-    def __init__(self, args, world, phase, min_targets, log):
+    def __init__(self, args, world, phase, min_targets, log, max_rounds=None):
         self.args, self.world, self.phase, self.min_targets = args, world, phase, min_targets
-        self.q = selfplay.TreeQueue(args.iters, args.games_per_gpu, max_move=100, node_cap=args.node_cap, log=log)
+        self.max_rounds = max_rounds
+        # slots for two rounds (as many as the arena holds, TreeQueue caps them): the next round's trees
+        # take the slots beside the current round's, not only those its finished trees free
+        self.q = selfplay.TreeQueue(args.iters, args.games_per_gpu, slots=2 * args.games_per_gpu, max_move=100,
+                                    node_cap=args.node_cap, log=log)
         self.pooled = 0
         self.speculated = 0
+        self.rnd = 0
+        self.rate = None          # pooled targets per tree of the rounds done (collect sets it)
+
+    def maybe_next(self, q):
+        rnd = self.rnd
+        if len(q.rounds) > rnd + 1 or (self.max_rounds is not None and rnd + 1 >= self.max_rounds):
+            return
+        walked, n = q.targets_so_far(rnd)
+        Q = q.rounds[rnd].Q
+        if walked >= max(1, int(Q * LOOKAHEAD_WALKED)):
+            rate = n / walked
+        elif self.rate is not None:          # the finished rounds' yield until this round's own estimate
+            rate = self.rate
+        else:
+            return
+        projected = self.pooled + rate * Q * self.world
+        if projected < 1.25 * self.min_targets:
+            q.add(round_seeds(self.args, self.world, self.phase, rnd + 1))
+            self.speculated += 1
 
     def round(self, rnd):
+        self.rnd = rnd
         while len(self.q.rounds) <= rnd:
             self.q.add(round_seeds(self.args, self.world, self.phase, len(self.q.rounds)))
-
-        def maybe_next(q):
-            if len(q.rounds) > rnd + 1:
-                return
-            walked, n = q.targets_so_far(rnd)
-            Q = q.rounds[rnd].Q
-            if walked < Q // 2:
-                return
-            projected = self.pooled + n / max(1, walked) * Q * self.world
-            if projected < 1.25 * self.min_targets:
-                q.add(round_seeds(self.args, self.world, self.phase, rnd + 1))
-                self.speculated += 1
-        self.q.run(rnd, on_slice=maybe_next)
+        self.q.run(rnd, on_slice=self.maybe_next)
         return self.q.result(rnd)
+
+    def drive(self):
+        """One slice of whatever the queue holds beyond the finished round
+        (collect calls it while a collective waits for slower ranks); False
+        when there is nothing to search."""
+        if self.q.idle():
+            return False
+        return self.q.step(on_slice=self.maybe_next)
 
     def close(self):
         self.q.close()
 
 
-def collect(rank, world, args, phase, min_targets, log):
+def collect(rank, world, args, phase, min_targets, log, max_rounds=None):
+    """get_mccfr_targets (train_from_scratch.py:45-64): data rounds of
+    `games_per_gpu` simulate_game trees per rank until the pooled targets
+    reach min_targets (or `max_rounds` rounds).  The per-round collectives
+    (the --on-error check, the target all-gathers) are async: while a slower
+    rank has not finished its round, this rank's host keeps driving the next
+    round's queue slices instead of blocking."""
     feats, values, tuples = [], [], []
     dropped = {k: 0 for k in selfplay.ERROR_CLASSES}
     pooled = 0
     rnd = 0
-    look = _Lookahead(args, world, phase, min_targets, log) if getattr(args, "lookahead", True) else None
-    while pooled < min_targets:
-        seeds = round_seeds(args, world, phase, rnd)
-        t0 = time.time()
-        if look is None:
-            b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap, log=log)
-        else:
-            look.pooled = pooled
-            b, stats, t = look.round(rnd)
-        counts, first_ref, first_eng = lane_errors(stats, t, seeds)
-        if args.on_error == "raise":
-            bad = torch.tensor([0 if first_ref is None else 1, 0 if first_eng is None else 1], device=stats.device)
-            if world > 1:
-                torch.distributed.all_reduce(bad)          # every rank stops together
-            if int(bad[0].item()):
-                raise TreeError("simulate_game raised in the search (first failing seed on this rank: %s; "
-                                "%d value errors, %d terminal positions)"
-                                % (first_ref, counts["value_error"], counts["terminal"]))
-            if int(bad[1].item()):
-                raise EngineCapacityError("a tree exceeded an engine capacity the reference does not have (first "
-                                          "seed on this rank: %s; %d capacity, %d pool)"
-                                          % (first_eng, counts["capacity"], counts["pool"]))
-        f, v = selfplay.all_gather_targets(t["feat"], t["value"])
-        feats.append(f.cpu())
-        values.append(v.cpu())
-        if args.save_tuples:
-            tuples += selfplay.targets_to_tuples(t)
-        pooled += f.shape[0]
-        for k in dropped:
-            dropped[k] += counts[k]
-        log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), dropped trees on rank %d: %d value "
-            "errors (the reference's ValueError), %d already-terminal positions, %d engine capacity, %d node pool, "
-            "%.1fs" % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, rank, counts["value_error"],
-                       counts["terminal"], counts["capacity"], counts["pool"], time.time() - t0))
-        rnd += 1
-    if look is not None:
-        look.close()
+    look = _Lookahead(args, world, phase, min_targets, log, max_rounds) if getattr(args, "lookahead", True) else None
+    drive = look.drive if look is not None else None
+    collect.round_done = []
+    try:
+        while pooled < min_targets and (max_rounds is None or rnd < max_rounds):
+            seeds = round_seeds(args, world, phase, rnd)
+            t0 = time.time()
+            if look is None:
+                b, stats, t = selfplay.simulate_games(seeds, args.iters, max_move=100, node_cap=args.node_cap,
+                                                      log=log)
+            else:
+                look.pooled = pooled
+                b, stats, t = look.round(rnd)
+            counts, first_ref, first_eng = lane_errors(stats, t, seeds)
+            if args.on_error == "raise":
+                bad = torch.tensor([0 if first_ref is None else 1, 0 if first_eng is None else 1],
+                                   device=stats.device)
+                if world > 1:                                  # every rank stops together
+                    selfplay.wait_driving(torch.distributed.all_reduce(bad, async_op=True), drive)
+                if int(bad[0].item()):
+                    raise TreeError("simulate_game raised in the search (first failing seed on this rank: %s; "
+                                    "%d value errors, %d terminal positions)"
+                                    % (first_ref, counts["value_error"], counts["terminal"]))
+                if int(bad[1].item()):
+                    raise EngineCapacityError("a tree exceeded an engine capacity the reference does not have "
+                                              "(first seed on this rank: %s; %d capacity, %d pool, %d unsupported)"
+                                              % (first_eng, counts["capacity"], counts["pool"],
+                                                 counts["unsupported"]))
+            f, v = selfplay.all_gather_targets(t["feat"], t["value"], drive=drive)
+            feats.append(f.cpu())
+            values.append(v.cpu())
+            if args.save_tuples:
+                tuples += selfplay.targets_to_tuples(t)
+            pooled += f.shape[0]
+            if look is not None:
+                look.rate = pooled / float((rnd + 1) * len(seeds) * world)
+            for k in dropped:
+                dropped[k] += counts[k]
+            collect.round_done.append(time.perf_counter())
+            log("phase %d round %d: %d trees/rank, %d pooled targets (%d/%d), dropped trees on rank %d: %d value "
+                "errors (the reference's ValueError), %d already-terminal positions, %d engine capacity, %d node "
+                "pool, %d unsupported branch / engine fault, %.1fs"
+                % (phase, rnd, len(seeds), f.shape[0], pooled, min_targets, rank, counts["value_error"],
+                   counts["terminal"], counts["capacity"], counts["pool"], counts["unsupported"], time.time() - t0))
+            rnd += 1
+    finally:
+        if look is not None:
+            look.close()
     collect.dropped = dropped
+    collect.rounds = rnd
     return torch.cat(feats), torch.cat(values), tuples
 
 

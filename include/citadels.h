@@ -51,17 +51,10 @@ typedef struct CitOption {
   uint64_t x;
 } CitOption;
 
-int cit_abi_version(void);              /* 8: cfr_pred as one launch with in-kernel leaf evaluation (cit_cfr_pred_fused, cit_mlp_*_wave); 7: diff rows as edge-slot runs (CfrNode.row), opponent edge runs that grow; 6: per-player card areas (hand / just-drawn / museum share 88 slots); 5: packed value-MLP path */
+int cit_abi_version(void);              /* 9: the card-area self-test moved to the test-only library (tests/testkit.py); 8: cfr_pred as one launch with in-kernel leaf evaluation (cit_cfr_pred_fused, cit_mlp_*_wave); 7: diff rows as edge-slot runs (CfrNode.row), opponent edge runs that grow; 6: per-player card areas (hand / just-drawn / museum share 88 slots); 5: packed value-MLP path */
 int cit_game_bytes(void);              /* row width of `games` */
 int cit_seer_scratch_words(void);      /* uint64 words of seer scratch per lane */
 int cit_layout(int* out, int n);       /* struct offsets, for binding self-checks */
-/* Self-test of the card-area list operations (csrc/cit_area_test.h): lane l
- * runs a pseudo-random sequence of n_ops list operations (seeds[l]) on its
- * game row (zeroed by the caller); log[l][i] records op i.  Tests compare the
- * rows and logs with the host build's. */
-int cit_area_test(void* games, uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int n_ops,
-                  uint32_t* log, hipStream_t stream);
-
 /* random.seed(seeds[l]) (CPython init_by_array) or, numpy_style != 0,
  * np.random.seed(seeds[l]) (init_genrand) for every lane. */
 int cit_mt_seed(uint32_t* mt, uint32_t* mt_idx, int B, const uint64_t* seeds, int numpy_style,

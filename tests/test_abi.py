@@ -32,7 +32,7 @@ def test_layout_matches(lib):
     assert list(out[:n]) == L.expected_layout()
     assert lib.cit_game_bytes() == L.GAME_BYTES
     assert lib.cit_seer_scratch_words() == L.SEER_MAX
-    assert lib.cit_abi_version() == 8
+    assert lib.cit_abi_version() == 9
 
 
 def test_cfr_pool_layout(lib):

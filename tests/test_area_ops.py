@@ -124,8 +124,8 @@ def test_host_area_ops_match_list_model():
 @pytest.mark.gpu
 def test_gpu_area_ops_match_host():
     import torch
-    from citadels_self_play_amd import _lib
-    lib = _lib.load()
+    import testkit
+    lib = testkit.lib()
     B = len(SEEDS)
     ref_games, ref_log = host_run(SEEDS, N_OPS)
     games = torch.zeros((B, L.GAME_BYTES), dtype=torch.uint8, device="cuda")
@@ -133,8 +133,8 @@ def test_gpu_area_ops_match_host():
     idx = torch.zeros(B, dtype=torch.int32, device="cuda")
     seeds = torch.as_tensor(np.asarray(SEEDS, np.uint64).view(np.int64), device="cuda")
     log = torch.zeros((B, N_OPS), dtype=torch.int32, device="cuda")
-    _lib.check(lib.cit_area_test(games.data_ptr(), mt.data_ptr(), idx.data_ptr(), B, seeds.data_ptr(), N_OPS,
-                                 log.data_ptr(), torch.cuda.current_stream().cuda_stream), "cit_area_test")
+    assert lib.citk_area_test(games.data_ptr(), mt.data_ptr(), idx.data_ptr(), B, seeds.data_ptr(), N_OPS,
+                              log.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     assert np.array_equal(log.cpu().numpy().view(np.uint32), ref_log)
     assert np.array_equal(games.cpu().numpy(), ref_games)

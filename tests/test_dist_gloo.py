@@ -75,3 +75,49 @@ def test_gloo_gather_shard_broadcast():
         m0 = models.ValueOnlyNN(418, 64)
         for k, v in m0.state_dict().items():
             assert np.array_equal(out[-1][4][k], v.numpy()), k
+
+
+def _driven_worker(rank, ws, port, q):
+    """Rank 0 reaches the all-gather first and drives a stand-in for its
+    queue's slices while rank 1 (late by 1.5 s) has not joined; the pooled
+    rows must be the blocking gather's."""
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from citadels_self_play_amd import selfplay
+        g = torch.Generator().manual_seed(rank)
+        n = [4, 2][rank]
+        feat = torch.randint(0, 9, (n, 418), generator=g).float()
+        value = torch.rand((n, 6), generator=g, dtype=torch.float64)
+        if rank == 1:
+            time.sleep(1.5)
+        calls = [0]
+
+        def drive():
+            calls[0] += 1
+            time.sleep(0.01)
+            return calls[0] < 10_000
+        pf, pv = selfplay.all_gather_targets(feat, value, drive=drive)
+        bf, bv = selfplay.all_gather_targets(feat, value)
+        q.put((rank, calls[0], bool(torch.equal(pf, bf) and torch.equal(pv, bv)), pf.shape[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_gather_drives_while_waiting():
+    """train_from_scratch.collect's async all-gathers: the rank that waits for
+    a slower rank keeps calling drive() (its next round's queue slices)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_driven_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(2)])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert out[0][1] >= 20, out        # rank 0 drove slices for most of rank 1's 1.5 s delay
+    assert all(o[2] and o[3] == 6 for o in out), out

@@ -44,7 +44,8 @@ run_step() {
     smoke)
       (cd "$R" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1) ;;
     bench)
-      (cd "$R" && timeout -k 10 900 python -u bench.py ${val//,/ } > "$O/bench.json" 2> "$O/bench.err") \
+      (cd "$R" && timeout -k 10 900 python -u bench.py --full-out "$O/bench_full.json" ${val//,/ } > "$O/bench.json" \
+        2> "$O/bench.err") \
         && { for f in /tmp/bench_trace_*/*/*kernel_stats.csv /tmp/bench_trace_*/*kernel_stats.csv; do
                [ -f "$f" ] && cp "$f" "$O/bench_rollout_kernel_stats.csv"; done; true; } ;;
     trace)

@@ -38,19 +38,32 @@ VARIANTS = {"top": (8, 9, 10, 11, 12, 14, 15), "node": (5, 6, 7), "engine": (0, 
             "sample": (5, 16, 17, 18, 19, 20), "rows": (7, 21, 22, 23), "pred": (8, 9, 10, 11, 12, 14, 24)}
 
 
+# PROF_TAG / PROF_FLAGS: a tagged set of variants built with extra flags (A/B of a
+# change inside one scope), e.g. PROF_TAG=base PROF_FLAGS="-DCIT_SHUFFLE_TRACE=0"
+TAG = os.environ.get("PROF_TAG", "")
+EXTRA = os.environ.get("PROF_FLAGS", "").split()
+
+
 def lib_of(name):
-    return os.path.join(OUT, "libcitprof_%s.so" % name)
+    return os.path.join(OUT, "libcitprof_%s%s.so" % (name, "_" + TAG if TAG else ""))
 
 
-def build():
+def build(only=None):
+    """Compile the variants in parallel (PROF_ONLY=name,name: a subset)."""
     import __graft_entry__ as G
     os.makedirs(OUT, exist_ok=True)
     others = [os.path.join(ROOT, "build", "hip", u.replace(".hip", ".o")) for u in G.HIP_UNITS if u != "cit_cfr.hip"]
-    for name, ids in VARIANTS.items():
-        mask = sum(1 << i for i in ids)
-        o = os.path.join(OUT, "cit_cfr_%s.o" % name)
-        subprocess.check_call([G.HIPCC] + G.HIP_FLAGS + ["-DCIT_PROF", "-DCIT_PROF_MASK=%dull" % mask, "-c",
-                                                          os.path.join(G.CSRC, "cit_cfr.hip"), "-o", o])
+    only = only or [n for n in os.environ.get("PROF_ONLY", "").split(",") if n]
+    names = [n for n in VARIANTS if not only or n in only]
+    procs = []
+    for name in names:
+        mask = sum(1 << i for i in VARIANTS[name])
+        o = os.path.join(OUT, "cit_cfr_%s%s.o" % (name, "_" + TAG if TAG else ""))
+        procs.append((name, o, subprocess.Popen([G.HIPCC] + G.HIP_FLAGS + EXTRA + [
+            "-DCIT_PROF", "-DCIT_PROF_MASK=%dull" % mask, "-c", os.path.join(G.CSRC, "cit_cfr.hip"), "-o", o])))
+    for name, o, p in procs:
+        if p.wait():
+            raise RuntimeError("hipcc failed for variant %s" % name)
         subprocess.check_call([G.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", o] + others + ["-o", lib_of(name)])
         print(lib_of(name))
 
@@ -88,7 +101,8 @@ def run(which=None, workloads=None):
     import citadels_self_play_amd._lib as LL
     from citadels_self_play_amd.engine import GameBatch, pool_caps
     which = None if which in ("", "all") else which
-    loads = [("plain", LL.LIB_PATH)] + [(n, lib_of(n)) for n in VARIANTS if which in (None, n)]
+    loads = [("plain", LL.LIB_PATH)] + [(n, lib_of(n)) for n in VARIANTS if which in (None, n) or
+                                        (which and n in which.split("+"))]
     plain = {}
     for vname, path in loads:
         LL._lib = None
@@ -115,7 +129,7 @@ def run(which=None, workloads=None):
             phases = {NAMES[i]: {"calls": int(cnt[i]), "cycles_per_call": cyc[i] / max(cnt[i], 1),
                                  "cycles_per_tree": cyc[i] / B, "cycles_per_carry": cyc[i] / max(st[:, 3].sum(), 1)}
                       for i in ids}
-            print(json.dumps({"variant": vname, "workload": tag, "trees": B, "iters": iters, "ms": ms,
+            print(json.dumps({"variant": vname + ("_" + TAG if TAG else ""), "workload": tag, "trees": B, "iters": iters, "ms": ms,
                               "ms_plain": plain.get(tag), "carry_outs": int(st[:, 3].sum()),
                               "nodes": int(st[:, 1].sum()), "phases": phases}), flush=True)
 

@@ -909,6 +909,11 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
                      "error_lanes_nonterminal": int(errs), "terminal_positions": int(terms), "leaf_rounds": rounds,
                      "error_classes": {k: int(v) for k, v in zip(selfplay.ERROR_CLASSES, ncls)},
                      "pooled_targets": n_targets})
+    # the reps' batches (config 5's one-round batch may hold its whole node arena) go before the next runs
+    b = stats = t = term = st = None
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
     streams = None
     if config == 3 and args.cfr_streams > 1:
         streams = _cfr_streams(args, world, rank, dev, iters, per_gpu, node_cap)
@@ -1164,6 +1169,9 @@ def main():
         line = {"pmc_child": 1}
         from citadels_self_play_amd import engine
         for key, c, n in PMC_CHILD_LEGS:
+            import gc                  # as the main run: each leg from an empty allocator cache, so a leg's
+            gc.collect()               # trees take the same path (tree queue or one launch) as its timed run
+            torch.cuda.empty_cache()
             before = engine.LAUNCHES.get(KERNELS[c], 0)
             r = run_cfr(c, args, 1, 0, dev, cpu=False, per_gpu=n, warm_rep=False, n_reps=1)
             m = r["median"]

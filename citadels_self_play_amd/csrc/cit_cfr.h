@@ -441,6 +441,46 @@ CIT_HD uint32_t* w_row(const CfrTree& T, int which) { return reinterpret_cast<ui
 #else
 #define CIT_NOINLINE inline
 #endif
+// CFR_INLINE_LEVEL: which of the search's wrappers are inlined into their
+// callers instead of called.  An out-of-line call on gfx950 waits for all of
+// the caller's memory operations at entry (s_waitcnt vmcnt(0) lgkmcnt(0)),
+// saves the VGPR that holds its spilled SGPRs to scratch and reloads it --
+// a scratch round trip -- before it returns; the search makes several such
+// calls per carry_out.  Inlining costs code size (each inlined wrapper is
+// copied to each call site).
+//   1: eng_prepare, eng_first_upto2 (per node, few call sites), cfr_update_regrets
+//      (per backprop level, one call site)
+//   2: + eng_carry, eng_list_reg (per carry_out / per listing)
+//   3: + cfr_node, eng_sample, eng_list
+//   4: + cfr_update_strategy, cfr_choose
+#ifndef CFR_INLINE_LEVEL
+#define CFR_INLINE_LEVEL 3
+#endif
+#if defined(__HIPCC__)
+#define CFR_INLINED __host__ __device__ inline __attribute__((always_inline))
+#else
+#define CFR_INLINED inline
+#endif
+#if CFR_INLINE_LEVEL >= 1
+#define CFR_INL1 CFR_INLINED
+#else
+#define CFR_INL1 CIT_NOINLINE
+#endif
+#if CFR_INLINE_LEVEL >= 2
+#define CFR_INL2 CFR_INLINED
+#else
+#define CFR_INL2 CIT_NOINLINE
+#endif
+#if CFR_INLINE_LEVEL >= 3
+#define CFR_INL3 CFR_INLINED
+#else
+#define CFR_INL3 CIT_NOINLINE
+#endif
+#if CFR_INLINE_LEVEL >= 4
+#define CFR_INL4 CFR_INLINED
+#else
+#define CFR_INL4 CIT_NOINLINE
+#endif
 
 // The search's two streams sit in its LDS block (CfrTree::py / np, device);
 // an engine call or a numpy draw works on a register copy of the stream's
@@ -455,7 +495,7 @@ CIT_HD auto cfr_with_np(CfrTree& T, F f) {
 }
 
 // option.carry_out on working row `which`, counted; returns the winner (-1: none)
-CIT_NOINLINE int eng_carry(CfrTree& T_in, int which, CitOpt o_in) {
+CFR_INL2 int eng_carry(CfrTree& T_in, int which, CitOpt o_in) {
   CIT_PROF_SCOPE(0);
   CfrTree& T = CFR_T(T_in);
   CitOpt o = cfr_uopt(o_in);
@@ -465,7 +505,7 @@ CIT_NOINLINE int eng_carry(CfrTree& T_in, int which, CitOpt o_in) {
   T.py = py;
   return w;
 }
-CIT_NOINLINE void eng_prepare(CfrTree& T_in, int which) {
+CFR_INL1 void eng_prepare(CfrTree& T_in, int which) {
   CIT_PROF_SCOPE(1);
   CfrTree& T = CFR_T(T_in);
   CitMT py = T.py;
@@ -485,7 +525,7 @@ struct CfrCnt {
 };
 CIT_HD CfrCnt cfr_ucnt(CfrCnt c) { return {cfr_u(c.n), cfr_u(c.err)}; }
 // Every option of working row `which` into T.optbuf (HBM, CFR_OPT_CAP).
-CIT_NOINLINE CfrCnt eng_list(CfrTree& T_in, int which) {
+CFR_INL3 CfrCnt eng_list(CfrTree& T_in, int which) {
   CIT_PROF_SCOPE(4);
   CfrTree& T = CFR_T(T_in);
   ListSink s(cfr_glb(T.optbuf), CFR_OPT_CAP);
@@ -521,7 +561,7 @@ struct CfrFirst {
   uint32_t err;
   CitOpt o;
 };
-CIT_NOINLINE CfrFirst eng_first_upto2(CfrTree& T_in, int which) {
+CFR_INL1 CfrFirst eng_first_upto2(CfrTree& T_in, int which) {
   CIT_PROF_SCOPE(2);
   CfrTree& T = CFR_T(T_in);
   const CitGame& g = cfr_w(T, cfr_u(which));
@@ -536,7 +576,7 @@ struct CfrRegList {
   uint32_t err;
   uint32_t r0, r1, r2, r3;
 };
-CIT_NOINLINE CfrRegList eng_list_reg(CfrTree& T_in, int which) {
+CFR_INL2 CfrRegList eng_list_reg(CfrTree& T_in, int which) {
   CIT_PROF_SCOPE(2);
   CfrTree& T = CFR_T(T_in);
   RegSink s;
@@ -552,7 +592,7 @@ __device__ __forceinline__ CitOpt cfr_reg_opt(const CfrRegList& L, int k) {
   return s.at(k);
 }
 #endif
-CIT_NOINLINE void eng_sample(CfrTree& T_in, int which, int orig, int role_sample) {
+CFR_INL3 void eng_sample(CfrTree& T_in, int which, int orig, int role_sample) {
   CIT_PROF_SCOPE(5);
   CfrTree& T = CFR_T(T_in);
   CitMT py = T.py;
@@ -962,7 +1002,7 @@ CIT_HD void opt_mutate(CitOpt& o, const CitGame& g) {
 // then a new node whose row is that game.  `skipped`: the caller already ran
 // skip_false_choice (the facade's CFRNode constructor), so it is not run
 // again.  Returns the node id (-1 on error).
-CIT_NOINLINE int cfr_node(CfrTree& T_in, int which, int parent, int depth, int skipped) {
+CFR_INL3 int cfr_node(CfrTree& T_in, int which, int parent, int depth, int skipped) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(7);
   which = cfr_u(which);
@@ -1310,7 +1350,7 @@ CIT_HD void cfr_expand(CfrTree& T, int n) {                        // :93-100
 }
 
 // ---------------------------------------------------------- strategies
-CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
+CFR_INL4 void cfr_update_strategy(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(11);               // :292-319
   n = cfr_u(n);
@@ -1422,7 +1462,7 @@ CIT_NOINLINE void cfr_update_strategy(CfrTree& T_in, int n) {
 }
 
 // action_choice(live=False) (:67-91): returns the edge index within the node
-CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
+CFR_INL4 int cfr_choose(CfrTree& T_in, int n) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(12);
   n = cfr_u(n);
@@ -1468,7 +1508,7 @@ CIT_NOINLINE int cfr_choose(CfrTree& T_in, int n) {
 
 // ------------------------------------------------------------- backup
 // (the node's header fields come from the caller's read of its record)
-CIT_NOINLINE void cfr_update_regrets(CfrTree& T_in, int n, int nch, int fe, int flags, int player) {
+CFR_INL1 void cfr_update_regrets(CfrTree& T_in, int n, int nch, int fe, int flags, int player) {
   CfrTree& T = CFR_T(T_in);
   CIT_PROF_SCOPE(13);                // :231-256
   n = cfr_u(n);

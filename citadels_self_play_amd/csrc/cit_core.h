@@ -479,7 +479,11 @@ CIT_HD uint32_t mt_next(CitMT& r) {
     r.win_base = -1;
 #elif defined(__HIP_DEVICE_COMPILE__)
     if (r.coop) {
-      mt_twist_coop((cit_lds_u32*)r.mt);
+      // (coop streams belong to one-wave workgroups: uniform_game launches 64 threads)
+      if (CIT_TWIST_INLINE)
+        mt_twist_wave((cit_lds_u32*)r.mt);
+      else
+        mt_twist_coop((cit_lds_u32*)r.mt);
       r.win_base = -1;
     } else {
       mt_twist(r);

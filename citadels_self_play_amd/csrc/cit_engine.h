@@ -357,53 +357,6 @@ CIT_HD void shuffle_seq(CitMT& rng, int n, At at) {
     at(j) = t;
   }
 }
-#if CIT_WAVE
-// random.shuffle for a coop stream with the swaps never applied one by one
-// (the determinization's deck: cit_sample_private_wave).  Fisher-Yates' draws
-// j_t (step t swaps i = n-1-t with j_t) do not depend on the data, so a scalar
-// pass draws them all first (the same draws in the same order); then each
-// lane traces its final position back through the swaps to where its element
-// started -- final position q >= 1 is written once, at step t = n-1-q, from
-// position j_t, and walking the earlier swaps backwards from there gives the
-// original index; position 0 walks every swap -- and one gather + one store
-// move the sequence.  The walk is lane compares and selects per swap, with no
-// memory latency in the chain.  n <= 128 and a coop stream, else shuffle_seq.
-template <class At>
-CIT_HD void shuffle_trace(CitMT& rng, int n, At at) {
-  if (!(rng.coop && n > 1 && n <= 128)) {
-    shuffle_seq(rng, n, at);
-    return;
-  }
-  CitMT w = cit_mt_window(rng);
-  const int l = cit_lane();
-  int jv0 = 0, jv1 = 0;                      // lane t: j_t (t < 64), lane t - 64: j_t (t >= 64)
-  for (int t = 0; t < n - 1; t++) {
-    const int j = __builtin_amdgcn_readfirstlane((int)mt_randbelow(w, (uint32_t)(n - t)));
-    jv0 = l == t ? j : jv0;
-    jv1 = l + 64 == t ? j : jv1;
-  }
-  // p0 / p1: where the element that ends at position l / 64 + l starts
-  int p0 = 0, p1 = 0;
-  for (int u = n - 2; u >= 0; u--) {
-    const int j = u < 64 ? __builtin_amdgcn_readlane(jv0, u) : __builtin_amdgcn_readlane(jv1, u - 64);
-    const int i = n - 1 - u;
-    const int s0 = p0 == i ? j : (p0 == j ? i : p0);
-    p0 = l < i ? s0 : (l == i ? j : p0);
-    if (n > 64) {
-      const int s1 = p1 == i ? j : (p1 == j ? i : p1);
-      p1 = l + 64 < i ? s1 : (l + 64 == i ? j : p1);
-    }
-  }
-  const int x0 = l < n ? (int)at(p0) : 0, x1 = l + 64 < n ? (int)at(p1) : 0;
-  if (l < n) at(l) = (uint8_t)x0;
-  if (l + 64 < n) at(l + 64) = (uint8_t)x1;
-  cit_mt_unwindow(rng, w);
-}
-#endif
-// the determinization's deck shuffle through shuffle_trace (0: shuffle_seq)
-#ifndef CIT_SHUFFLE_TRACE
-#define CIT_SHUFFLE_TRACE 1
-#endif
 CIT_HD void shuffle_arr(CitMT& rng, uint8_t* a, int n) {
   shuffle_seq(rng, n, [a](int i) -> uint8_t& { return a[i]; });
 }
@@ -2503,14 +2456,7 @@ CIT_HD void kr_strip(const CitGame& g, uint16_t* kr, int role) {
 #endif
 static_assert(CIT_SAMPLE_SCRATCH >= 880 && CIT_SAMPLE_SCRATCH % 16 == 0, "determinization scratch");
 
-// the opponents' new hands in one lane pass when they fit 64 lanes (see
-// cit_sample_private_wave); 0: one wave_append per player
-#ifndef CIT_DEAL_BATCHED
-#define CIT_DEAL_BATCHED 1
-#endif
 #if CIT_WAVE
-// bits [0, k) of a lane mask (k in [0, 64])
-CIT_HD uint64_t cit_lowmask(int k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
 // Append src(i), i < cnt (<= 128), to dst[base..) skipping CIT_NO_CARD (the
 // reference's add_card drops the "Deck Empty" sentinel); returns the count
 // appended.  Lanes i and 64 + i move one element each.
@@ -2628,11 +2574,7 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
       kk = ll < n ? ll : n;
       n -= kk;
     }
-#if CIT_SHUFFLE_TRACE
-    shuffle_trace(w, nu, [unk](int i) -> uint8_t& { return unk[i]; });
-#else
     shuffle_arr(w, unk, nu);
-#endif
     __syncthreads();
     int m = n < nu ? n : nu;
     // the known cards, then the shuffled unknowns: one compaction pass
@@ -2685,77 +2627,9 @@ CIT_HD void cit_sample_private_wave(CitGame& g, int orig, bool role_sample, CitM
         if (rid < rr) strip(cit_readlane(rl, rid));
     }
   }
-  // sample_cards_for_opponent (:264-280) draws nothing, so every opponent's new
-  // hand can be dealt before the role draws below (which read no hand).  When
-  // all the new hands together fit the wave's 64 lanes (the usual case), they
-  // are dealt in one pass: player p's known cards, then unknowns
-  // unk[head_p ..), at lanes [off_p, off_p + cnt_p); each lane finds its player
-  // among the (<= 5) segment starts, and the "Deck Empty" sentinels are
-  // compacted out per segment.  Longer hands take the per-player loop.
-  bool dealt = false;
-#if CIT_DEAL_BATCHED
-  {
-    int kkp[CIT_NP], hop[CIT_NP], hdp[CIT_NP], offp[CIT_NP], cntp[CIT_NP];
-    int tot = 0, hd = head;
-#pragma unroll
-    for (int p = 0; p < CIT_NP; p++) {
-      int n = g.pl[p].n_hand, ho = 0, kk = 0;
-      if (p != orig) {
-        const uint64_t hm = cit_ballot(uu && ktarget == p);
-        if (hm) {
-          const int e = __ffsll((unsigned long long)hm) - 1;
-          const int hl = cit_readlane(klen, e);
-          ho = cit_readlane(koff, e);
-          kk = hl < n ? hl : n;
-          n -= kk;
-        }
-      }
-      const int m = p == orig ? 0 : (n < nu - hd ? n : nu - hd);
-      kkp[p] = kk;
-      hop[p] = ho;
-      hdp[p] = hd;
-      offp[p] = tot;
-      cntp[p] = p == orig ? 0 : kk + m;
-      tot += cntp[p];
-      hd += m;
-    }
-    if (tot <= 64) {
-      dealt = true;
-      int pq = 0;
-#pragma unroll
-      for (int p = 1; p < CIT_NP; p++) pq = l >= offp[p] ? p : pq;
-      int kk = kkp[0], ho = hop[0], hh = hdp[0], of = offp[0];
-#pragma unroll
-      for (int p = 1; p < CIT_NP; p++)
-        if (pq == p) {
-          kk = kkp[p];
-          ho = hop[p];
-          hh = hdp[p];
-          of = offp[p];
-        }
-      const int i = l - of;
-      const bool on = l < tot;
-      const int a = g.kh_pool[on && i < kk ? ho + i : 0], b = unk[on && i >= kk ? hh + i - kk : 0];
-      const int c = on ? (i < kk ? a : b) : CIT_NO_CARD;
-      const uint64_t vm = cit_ballot(c != CIT_NO_CARD);
-      // this lane's segment [of, l) of valid lanes: its slot in the player's new hand
-      const uint64_t seg_below = below & ~cit_lowmask(of);
-      if (c != CIT_NO_CARD) g.pl[pq].hand[__popcll(vm & seg_below)] = (uint8_t)c;
-      head = hd;
-#pragma unroll
-      for (int p = 0; p < CIT_NP; p++) {
-        if (p == orig) continue;
-        const int hi = offp[p] + cntp[p];
-        const uint64_t segm = cit_lowmask(hi) & ~cit_lowmask(offp[p]);
-        const int nh = __popcll(vm & segm), n_old = g.pl[p].n_hand;
-        if (nh < n_old) area_splice(g, g.pl[p], AL_HAND, nh, n_old - nh, 0, [](int) { return 0; });
-      }
-    }
-  }
-#endif
   for (int p = 0; p < CIT_NP; p++) {
     CitPlayer& Q = g.pl[p];
-    if (p != orig && !dealt) {   // sample_cards_for_opponent (:264-280): known cards, then unknowns, one pass
+    if (p != orig) {   // sample_cards_for_opponent (:264-280): known cards, then unknowns, one pass
       int n = Q.n_hand, ho = 0, kk = 0;
       uint64_t hm = cit_ballot(uu && ktarget == p);
       if (hm) {

@@ -98,6 +98,7 @@ SALU_PEAK = N_CU * CLOCK_HZ  # one scalar instruction per clock per CU
 BASE_SEED = 1_000_000_000
 CFR_SEED = 30_000_000        # configs 3-5: positions / trees seeded from here (tools/bench_selfplay.py)
 KERNELS = {2: "k_rollout_u", 3: "k_cfr_decide", 4: "k_cfr_pred_fused", 5: "k_cfr_train_slice"}
+SEARCH_KERNELS = ("k_cfr_decide", "k_cfr_pred_fused", "k_cfr_train_slice", "k_cfr_pred_step")
 # The reference's own Python, BASELINE.md §2 config 1 (survey container, 8-core Xeon).
 REF_PY = {"1_core": 12301, "8_procs": 83869, "unit": "carry_out transitions/s",
           "where": "survey container (BASELINE.md), not this box"}
@@ -352,17 +353,22 @@ def _child_line(logp):
 def _by_leg(per_kernel, child):
     """{kernel: {dispatch id: value}} -> {leg key: [values of its launches]}:
     the child runs PMC_CHILD_LEGS in order and reports each leg's launches of
-    its search kernel, so a kernel's dispatches, in dispatch order, go to those
-    legs in turn (later dispatches -- e.g. config 5's overflow retries, which
-    launch k_cfr_decide -- to none)."""
+    every search kernel (a config-5 leg searches through the tree queue's
+    k_cfr_train_slice, or through k_cfr_decide when its trees fit at once; an
+    overflowed tree is searched again by k_cfr_decide), so a kernel's
+    dispatches, in dispatch order, go to the legs in turn."""
     taken, out = {}, {}
     for key, c, _ in PMC_CHILD_LEGS:
-        k = KERNELS[c]
-        ids = sorted(per_kernel.get(k, {}))
-        n = int(child[key]["launches"])
-        mine = ids[taken.get(k, 0):taken.get(k, 0) + n]
-        taken[k] = taken.get(k, 0) + n
-        out[key] = [per_kernel[k][i] for i in mine]
+        launches = child[key]["launches"]
+        if not isinstance(launches, dict):          # (an older child line: its own kernel only)
+            launches = {KERNELS[c]: launches}
+        vals = []
+        for k, n in launches.items():
+            ids = sorted(per_kernel.get(k, {}))
+            mine = ids[taken.get(k, 0):taken.get(k, 0) + int(n)]
+            taken[k] = taken.get(k, 0) + int(n)
+            vals += [per_kernel[k][i] for i in mine]
+        out[key] = vals
     return out
 
 
@@ -385,7 +391,7 @@ def _pmc_pass(counters, outdir, config=2, timeout_s=150, cfr_child=False):
         child = _child_line(logp)
         per_kernel = {}
         for r in rows:
-            k = next((k for k in set(KERNELS.values()) if k in r.get("Kernel_Name", "")), None)
+            k = next((k for k in SEARCH_KERNELS if k in r.get("Kernel_Name", "")), None)
             if k is not None and "Dispatch_Id" in r:
                 d = per_kernel.setdefault(k, {}).setdefault(int(r["Dispatch_Id"]), {})
                 d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -505,7 +511,7 @@ def trace_in_run_cfr(timeout_s=300):
         for r in rows:
             name = r.get("Kernel_Name", "")
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
-            k = next((k for k in set(KERNELS.values()) if k in name), None)
+            k = next((k for k in SEARCH_KERNELS if k in name), None)
             if k is not None:
                 per_kernel.setdefault(k, {})[int(r["Dispatch_Id"])] = dur
             m = next((m for m in MLP_KERNELS if m in name), None)
@@ -515,7 +521,8 @@ def trace_in_run_cfr(timeout_s=300):
         for key, durs in _by_leg(per_kernel, child_line).items():
             if durs:
                 out[key] = {"launches": len(durs), "kernel_ms_total": float(sum(durs)),
-                            "kernel_avg_ms": float(sum(durs) / len(durs)), "carry_outs": child_line[key]["carry_outs"]}
+                            "kernel_avg_ms": float(sum(durs) / len(durs)), "carry_outs": child_line[key]["carry_outs"],
+                            "kernels": child_line[key]["launches"]}
         if mlp and child_line.get("mlp"):
             calls = int(child_line["mlp"]["calls"])
             out["mlp"] = {"calls": calls, "rows": child_line["mlp"]["rows"],
@@ -951,7 +958,9 @@ def run_cfr(config, args, world, rank, dev, pmc=None, cpu=True, per_gpu=None, wa
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                 "note": "no SQ counters for this leg: SURVEY §8(d)'s notional HBM figure"}
-    roof.update({"kernel": KERNELS[config], "issue": issue, "hbm_notional": hbm_notional, "pmc": pmc,
+    kern = "+".join(sorted((trace or {}).get("kernels") or {})) if isinstance((trace or {}).get("kernels"), dict) \
+        else KERNELS[config]
+    roof.update({"kernel": kern or KERNELS[config], "issue": issue, "hbm_notional": hbm_notional, "pmc": pmc,
                  "search_ms": ms})
     out = {"config": config, "workload": {
         3: "config3: %d positions per GPU (preset game + U[0,300] random steps), one cfr_train(200) decision each"
@@ -1034,7 +1043,9 @@ def _cfg5_rounds(args, world, rank, dev, iters, per_gpu):
     run, the first round's ramp and the last round's tail included."""
     from types import SimpleNamespace
     from citadels_self_play_amd import train_from_scratch as tfs
-    R = args.cfg5_rounds
+    # the same trees whatever the round size (5@960 runs twice the rounds of 1,920-tree ones), so the
+    # first round's ramp and the last round's tail weigh the same in every leg
+    R = max(args.cfg5_rounds, -(-args.cfg5_rounds * args.cfg5_trees // per_gpu))
     targs = SimpleNamespace(iters=iters, games_per_gpu=per_gpu, node_cap=None, seed=CFR_SEED + 90_000_000,
                             on_error="drop", save_tuples=False, lookahead=True)
     torch.cuda.synchronize()
@@ -1172,11 +1183,12 @@ def main():
             import gc                  # as the main run: each leg from an empty allocator cache, so a leg's
             gc.collect()               # trees take the same path (tree queue or one launch) as its timed run
             torch.cuda.empty_cache()
-            before = engine.LAUNCHES.get(KERNELS[c], 0)
+            before = dict(engine.LAUNCHES)
             r = run_cfr(c, args, 1, 0, dev, cpu=False, per_gpu=n, warm_rep=False, n_reps=1)
             m = r["median"]
             line[key] = {"carry_outs": m["carry_out_per_s"] * m["seconds"], "search_ms": m["seconds"] * 1e3,
-                         "launches": engine.LAUNCHES.get(KERNELS[c], 0) - before}
+                         "launches": {k: engine.LAUNCHES.get(k, 0) - before.get(k, 0) for k in SEARCH_KERNELS
+                                      if engine.LAUNCHES.get(k, 0) - before.get(k, 0)}}
         if not args.no_mlp:
             m = run_mlp(dev, calls=10, warm=2)
             line["mlp"] = {"calls": 12, "rows": m["rows"]}

@@ -4,7 +4,6 @@
 // tests/testkit.py binds it.
 #include <hip/hip_runtime.h>
 
-#define CIT_SHUFFLE_REG 1      // as the rollout unit (cit_hip.hip) builds the engine
 #include "cit_area_test.h"
 
 namespace {
@@ -39,9 +38,101 @@ __global__ __launch_bounds__(64) void k_area_test(uint32_t* games, uint32_t* mt,
   for (int i = threadIdx.x; i < kRowW; i += blockDim.x) games[l * kRowW + i] = row[i];
 }
 
+// Cycle microbenchmark of random.shuffle's building blocks on one wave with
+// an LDS stream (the search's determinization deck: ~60 unknown cards):
+// mode 0 the n - 1 draws alone, 1 draws + serial LDS swaps (the engine's coop
+// path), 2 draws + swaps in two VGPRs (CIT_SHUFFLE_REG), 3 draws first, then
+// each lane traces its final position back through the swaps (round 6's
+// rejected variant).  out[blk] = clock64 cycles per shuffle, averaged over
+// `reps`; sink[blk] keeps the results live.
+__global__ __launch_bounds__(64) void k_bench_shuffle(int mode, int n, int reps, unsigned long long* out,
+                                                       uint32_t* sink) {
+  __shared__ uint32_t mts[CIT_MT_N];
+  __shared__ uint8_t arr[128];
+  const int l = (int)threadIdx.x;
+  for (int i = l; i < CIT_MT_N; i += 64) mts[i] = 0x9e3779b9u * (uint32_t)(i + 1 + 977 * blockIdx.x);
+  if (l < 128) arr[l] = (uint8_t)l;
+  if (l + 64 < 128) arr[l + 64] = (uint8_t)(l + 64);
+  __syncthreads();
+  CitMT r;
+  r.mt = mts;
+  r.stride = 1;
+  r.pos = 0;
+  r.coop = CIT_MT_WINDOW;
+  r.win = 0;
+  r.win_base = -1;
+  uint32_t acc = 0;
+  mode = __builtin_amdgcn_readfirstlane(mode);
+  n = __builtin_amdgcn_readfirstlane(n);
+  const unsigned long long t0 = clock64();
+  for (int rep = 0; rep < reps; rep++) {
+    // the search keeps a stream's position and window base in SGPRs (its
+    // arguments are re-uniformised); say so here too
+    r.pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.pos);
+    r.win_base = __builtin_amdgcn_readfirstlane(r.win_base);
+    if (mode == 0) {
+      for (int i = n - 1; i > 0; i--) acc += mt_randbelow(r, (uint32_t)(i + 1));
+    } else if (mode == 1) {
+      for (int i = n - 1; i > 0; i--) {
+        const int j = (int)mt_randbelow(r, (uint32_t)(i + 1));
+        const uint8_t t = arr[i];
+        arr[i] = arr[j];
+        arr[j] = t;
+      }
+    } else if (mode == 2) {
+      int v0 = l < n ? arr[l] : 0, v1 = l + 64 < n ? arr[l + 64] : 0;
+      for (int i = n - 1; i > 0; i--) {
+        const int j = __builtin_amdgcn_readfirstlane((int)mt_randbelow(r, (uint32_t)(i + 1)));
+        const int x = i < 64 ? __builtin_amdgcn_readlane(v0, i) : __builtin_amdgcn_readlane(v1, i - 64);
+        const int y = j < 64 ? __builtin_amdgcn_readlane(v0, j) : __builtin_amdgcn_readlane(v1, j - 64);
+        v0 = l == i ? y : (l == j ? x : v0);
+        v1 = l + 64 == i ? y : (l + 64 == j ? x : v1);
+      }
+      if (l < n) arr[l] = (uint8_t)v0;
+      if (l + 64 < n) arr[l + 64] = (uint8_t)v1;
+    } else {
+      int jv0 = 0, jv1 = 0;
+      for (int t = 0; t < n - 1; t++) {
+        const int j = __builtin_amdgcn_readfirstlane((int)mt_randbelow(r, (uint32_t)(n - t)));
+        jv0 = l == t ? j : jv0;
+        jv1 = l + 64 == t ? j : jv1;
+      }
+      int p0 = 0, p1 = 0;
+      for (int u = n - 2; u >= 0; u--) {
+        const int j = u < 64 ? __builtin_amdgcn_readlane(jv0, u) : __builtin_amdgcn_readlane(jv1, u - 64);
+        const int i = n - 1 - u;
+        const int s0 = p0 == i ? j : (p0 == j ? i : p0);
+        p0 = l < i ? s0 : (l == i ? j : p0);
+        const int s1 = p1 == i ? j : (p1 == j ? i : p1);
+        p1 = l + 64 < i ? s1 : (l + 64 == i ? j : p1);
+      }
+      const int x0 = l < n ? arr[p0] : 0, x1 = l + 64 < n ? arr[p1] : 0;
+      if (l < n) arr[l] = (uint8_t)x0;
+      if (l + 64 < n) arr[l + 64] = (uint8_t)x1;
+    }
+  }
+  const unsigned long long t1 = clock64();
+  __syncthreads();
+  if (l == 0) {
+    out[blockIdx.x] = (t1 - t0) / (unsigned long long)(reps > 0 ? reps : 1);
+    uint32_t h = acc;
+    for (int i = 0; i < n; i++) h = h * 31u + arr[i];
+    sink[blockIdx.x] = h;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// k_bench_shuffle over `blocks` one-wave workgroups (out / sink: [blocks])
+int citk_bench_shuffle(int mode, int n, int reps, int blocks, unsigned long long* out, uint32_t* sink,
+                       hipStream_t stream) {
+  if (n < 2 || n > 128 || reps < 1 || blocks < 1 || !out || !sink) return -1;
+  hipLaunchKernelGGL(k_bench_shuffle, dim3(blocks), dim3(64), 0, stream, mode, n, reps, out, sink);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
 
 // lane l runs a pseudo-random sequence of n_ops list operations (seeds[l]) on
 // its game row (zeroed by the caller); log[l][i] records op i

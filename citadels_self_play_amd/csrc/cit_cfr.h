@@ -291,6 +291,14 @@ CIT_HD CitOpt cfr_uopt(const CitOpt& o) { return o; }
 // functions receive are then only the host build's.  Host: the pointers
 // bound in CfrTree.
 #if defined(__HIPCC__)
+// Invariant (cfr_leaf_eval): the in-kernel leaf evaluation's scratch overlays
+// w[0..1], lbuf, sbuf and cbuf, so nothing may read those after a leaf
+// evaluation before writing them again: the working rows are reloaded by the
+// next expansion, the list buffer refilled by the next listing, and the
+// strategy copies are valid only for node `cnode`, which the evaluation
+// resets to -1.  CFR_DEBUG_POISON builds overwrite all four with a pattern
+// after each evaluation so that a reader that breaks this fails the
+// fused-vs-rounds and golden tests.
 struct CfrLds {
   uint32_t w[2][CIT_GAME_BYTES / 4];
   CitOpt lbuf[CFR_LBUF];
@@ -1861,6 +1869,15 @@ CIT_NOINLINE int cfr_pred_run(CfrTree& T_in, CfrState& S_in, int iters, int max_
           double* pred = cfr_pred_of(T, n);
           for (int k = 0; k < 6; k++) pred[k] = (double)(5.0f * pr[k]);   // as the CP_WAIT resumption
           cfr_node(T, n).flags |= NF_PRED;
+#ifdef CFR_DEBUG_POISON
+          {   // (see CfrLds: nothing reads the overlaid buffers after an evaluation)
+            uint32_t* o = &cfr_ls.w[0][0];
+            const int nw = (int)((offsetof(CfrLds, cbuf) + sizeof(cfr_ls.cbuf) - offsetof(CfrLds, w)) / 4);
+            CFR_SYNC();
+            for (int i = CFR_LANE; i < nw; i += CFR_TEAM) o[i] = 0xDEADBEEFu;
+            CFR_SYNC();
+          }
+#endif
         } else
 #endif
         {

@@ -76,6 +76,10 @@ def round_seeds(args, world, phase, rnd):
 # fraction of the round is walked (round 5 waited for half, leaving the slots of
 # the earliest finished trees idle until then)
 LOOKAHEAD_WALKED = float(os.environ.get("CIT_LOOKAHEAD_WALKED", str(1.0 / 8)))
+# rounds the queue may hold beyond the one collect waits for: with one, a round that
+# fills every slot (960 trees per GPU: 1,920 slots) leaves the slots its tail frees
+# idle until collect moves on, so the rounds finished in pairs
+LOOKAHEAD_DEPTH = int(os.environ.get("CIT_LOOKAHEAD_DEPTH", "2"))
 
 
 class _Lookahead:
@@ -102,20 +106,26 @@ class _Lookahead:
         self.rate = None          # pooled targets per tree of the rounds done (collect sets it)
 
     def maybe_next(self, q):
-        rnd = self.rnd
-        if len(q.rounds) > rnd + 1 or (self.max_rounds is not None and rnd + 1 >= self.max_rounds):
+        """Add round last + 1 (last: the newest round in the queue, up to
+        LOOKAHEAD_DEPTH past the one collect waits for) once 1/8 of round
+        `last` is walked, if the rounds in flight project short of min_targets."""
+        rnd, last = self.rnd, len(q.rounds) - 1
+        if last - rnd >= LOOKAHEAD_DEPTH or (self.max_rounds is not None and last + 1 >= self.max_rounds):
             return
-        walked, n = q.targets_so_far(rnd)
-        Q = q.rounds[rnd].Q
-        if walked >= max(1, int(Q * LOOKAHEAD_WALKED)):
+        walked, n = q.targets_so_far(last)
+        Q = q.rounds[last].Q
+        if walked < max(1, int(Q * LOOKAHEAD_WALKED)):
+            if last > rnd or self.rate is None:
+                return
+            rate = self.rate                 # the finished rounds' yield until this round's own estimate
+        elif last == rnd:
             rate = n / walked
-        elif self.rate is not None:          # the finished rounds' yield until this round's own estimate
-            rate = self.rate
-        else:
-            return
-        projected = self.pooled + rate * Q * self.world
+        else:                                # the finished rounds' yield, else the current round's so far
+            w0, n0 = q.targets_so_far(rnd)
+            rate = self.rate if self.rate is not None else n0 / max(1, w0)
+        projected = self.pooled + rate * Q * self.world * (last - rnd + 1)
         if projected < 1.25 * self.min_targets:
-            q.add(round_seeds(self.args, self.world, self.phase, rnd + 1))
+            q.add(round_seeds(self.args, self.world, self.phase, last + 1))
             self.speculated += 1
 
     def round(self, rnd):
@@ -151,6 +161,7 @@ def collect(rank, world, args, phase, min_targets, log, max_rounds=None):
     look = _Lookahead(args, world, phase, min_targets, log, max_rounds) if getattr(args, "lookahead", True) else None
     drive = look.drive if look is not None else None
     collect.round_done = []
+    collect.queue = None
     try:
         while pooled < min_targets and (max_rounds is None or rnd < max_rounds):
             seeds = round_seeds(args, world, phase, rnd)
@@ -195,6 +206,10 @@ def collect(rank, world, args, phase, min_targets, log, max_rounds=None):
             rnd += 1
     finally:
         if look is not None:
+            q = look.q
+            collect.queue = {"slots": q.S, "overcommit": q.overcommit, "slices": q.n_slices,
+                             "paused_tree_slices": 0 if q.planner is None else q.planner.paused_slices,
+                             "speculated_rounds": look.speculated}
             look.close()
     collect.dropped = dropped
     collect.rounds = rnd

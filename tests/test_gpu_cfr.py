@@ -145,16 +145,20 @@ def test_gpu_cfr_strategy_lds_equals_hbm_path():
                 assert ea[fe:fe + nch]["child"].tobytes() == eh[fe:fe + nch]["child"].tobytes(), (l, i)
 
 
-def test_gpu_cfr_streams_overlap():
-    """Config-3 batches searched on two HIP streams at once (bench.py's
+@pytest.mark.parametrize("shape", [(4, 256, 2), (12, 1024, 3)], ids=["4x256_2streams", "timed_12x1024_3streams"])
+def test_gpu_cfr_streams_overlap(shape):
+    """Config-3 batches searched on HIP streams at once (bench.py's
     continuous loop) equal the same batches searched one after another:
-    decisions, stats, root games and both streams, bit for bit."""
-    from citadels_self_play_amd.engine import GameBatch
+    decisions, stats, root games and both streams, bit for bit -- at a small
+    shape and at the timed one (12 batches of 1,024 positions on the bench's
+    3 streams, engine.side_streams)."""
+    from citadels_self_play_amd.engine import GameBatch, side_streams
+    K, B, S = shape
 
     def make():
         bs = []
-        for k in range(4):
-            b = GameBatch(np.arange(9_000_000 + 1000 * k, 9_000_000 + 1000 * k + 256), preset=True)
+        for k in range(K):
+            b = GameBatch(np.arange(9_000_000 + 10_000 * k, 9_000_000 + 10_000 * k + B), preset=True)
             b.advance_random(0, 300)
             b.seed_numpy()
             b._pool(4096, 5 * 4096)
@@ -170,10 +174,10 @@ def test_gpu_cfr_streams_overlap():
     alone = make()
     ref = grab(alone, [b._cfr_decide(200, 4096, 5 * 4096) for b in alone])
     over = make()
-    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    sts = side_streams(torch.device("cuda"), S)
     res = []
     for k, b in enumerate(over):
-        with torch.cuda.stream(sts[k % 2]):
+        with torch.cuda.stream(sts[k % S]):
             res.append(b._cfr_decide(200, 4096, 5 * 4096))
     got = grab(over, res)
     for a, g in zip(ref, got):

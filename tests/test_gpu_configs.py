@@ -131,6 +131,24 @@ def test_gpu_train_from_scratch_on_error(tmp_path):
     assert T.collect.dropped["value_error"] >= 1 and T.collect.dropped["capacity"] == 0
 
 
+@pytest.mark.timeout(300)
+def test_gpu_collect_lookahead_equals_round_by_round():
+    """collect's cross-round queue (up to LOOKAHEAD_DEPTH rounds beyond the
+    one it waits for) pools exactly the targets of its rounds searched one
+    after another by simulate_games."""
+    from types import SimpleNamespace
+    from citadels_self_play_amd import train_from_scratch as T
+    base = dict(iters=300, games_per_gpu=16, node_cap=None, seed=CFG5_SEED0, on_error="drop", save_tuples=False)
+    out = {}
+    for la in (False, True):
+        f, v, _ = T.collect(0, 1, SimpleNamespace(lookahead=la, **base), 0, 10 ** 15, lambda m: None, max_rounds=4)
+        out[la] = (f.numpy(), v.numpy(), dict(T.collect.dropped), T.collect.queue)
+    assert out[False][0].shape[0] > 0
+    assert np.array_equal(out[False][0], out[True][0]) and np.array_equal(out[False][1], out[True][1])
+    assert out[False][2] == out[True][2]
+    assert out[True][3]["speculated_rounds"] == 3              # rounds 1-3 entered the queue ahead of collect
+
+
 @pytest.fixture(scope="module")
 def net():
     from citadels_self_play_amd import models

@@ -1,5 +1,5 @@
 """Config 5 through train_from_scratch.collect at one admission setting
-(CIT_LOOKAHEAD_WALKED, read at import): R rounds of N trees per GPU at
+(CIT_LOOKAHEAD_WALKED / CIT_LOOKAHEAD_DEPTH, read at import): R rounds of N trees per GPU at
 cfr_train(ITERS); one JSON line with the rounds' completion times."""
 import json
 import os
@@ -18,9 +18,12 @@ args = SimpleNamespace(iters=ITERS, games_per_gpu=N, node_cap=None, seed=30_000_
                        save_tuples=False, lookahead=True)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-feat, value, _ = tfs.collect(0, 1, args, 0, 10 ** 15, lambda m: None, max_rounds=R)
+T0 = time.perf_counter()
+log = (lambda m: print("%8.2f %s" % (time.perf_counter() - T0, m), flush=True)) if os.environ.get("CIT_LOG") else (
+    lambda m: None)
+feat, value, _ = tfs.collect(0, 1, args, 0, 10 ** 15, log, max_rounds=R)
 torch.cuda.synchronize()
 el = time.perf_counter() - t0
-print(json.dumps({"walked": tfs.LOOKAHEAD_WALKED, "trees": N, "rounds": R, "seconds": el,
+print(json.dumps({"walked": tfs.LOOKAHEAD_WALKED, "depth": tfs.LOOKAHEAD_DEPTH, "trees": N, "rounds": R, "seconds": el,
                   "trees_per_s": N * R / el, "round_done_s": [t - t0 for t in tfs.collect.round_done],
-                  "targets": int(feat.shape[0])}), flush=True)
+                  "targets": int(feat.shape[0]), "queue": tfs.collect.queue}), flush=True)

@@ -7,7 +7,7 @@
 //     measured).  Rows in LDS at an odd-dword stride, MT19937 words in HBM
 //     (structure of arrays).
 //   * k_cfr_target_count / k_cfr_targets: pre-order walks of finished MCCFR
-//     trees, one tree per lane.
+//     trees, one tree per lane (CFR_WALK_TPW trees per wave).
 #define CIT_NO_WAVE 1
 #include <hip/hip_runtime.h>
 
@@ -68,10 +68,23 @@ __global__ void k_rollout(uint32_t* games, uint32_t* mt, uint32_t* idx, uint64_t
   stage_out(lds, games, g0, nrows);
 }
 
+// Trees per wavefront of the two walks: lanes walking different trees diverge
+// (their pre-orders have different shapes), so a wave of 64 trees costs about
+// the sum of its trees' walks, and B / 64 waves leave most of the chip idle;
+// with one tree per wave the B walks run side by side (CFR_WALK_TPW=64: the
+// packed launch, for A/B).
+#ifndef CFR_WALK_TPW
+#define CFR_WALK_TPW 1
+#endif
+static_assert(CFR_WALK_TPW >= 1 && CFR_WALK_TPW <= 64, "trees per wave of the walks");
+__device__ __forceinline__ long walk_tree() {
+  return threadIdx.x < CFR_WALK_TPW ? (long)blockIdx.x * CFR_WALK_TPW + threadIdx.x : -1;
+}
+
 __global__ void k_cfr_target_count(uint8_t* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
                                    int32_t* counts) {
-  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= B) return;
+  long l = walk_tree();
+  if (l < 0 || l >= B) return;
   if (roots[l] < 0) {
     counts[2 * l] = counts[2 * l + 1] = 0;
     return;
@@ -84,10 +97,10 @@ __global__ void k_cfr_targets(uint8_t* pool, int B, int node_cap, int edge_cap, 
                               uint32_t* mt,
                               uint32_t* idx, const int32_t* offsets, int32_t* meta, float* feat, double* value,
                               double* dist, float* opt_feat) {
-  long l = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long l = walk_tree();
   // a lane without a tree touches nothing: the tree queue walks finished trees while
   // the other lanes' searches run (and write their own stream positions) on another stream
-  if (l >= B || roots[l] < 0) return;
+  if (l < 0 || l >= B || roots[l] < 0) return;
   CfrTree T = cfr_tree_view(pool, B, l, node_cap, edge_cap);
   CitMT r = lane_mt(mt, idx, B, l);
   cfr_emit_targets(T, r, roots[l], mode, (int)l, offsets[2 * l], offsets[2 * l + 1], meta, feat, value, dist, opt_feat);
@@ -181,7 +194,7 @@ int cit_get_options_lanes(void* games, uint32_t* mt, uint32_t* mt_idx, uint64_t*
 int cit_cfr_target_count(void* pool, int B, int node_cap, int edge_cap, const int32_t* roots, int mode,
                          int32_t* counts, hipStream_t stream) {
   if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !counts || mode < 0 || mode > 3) return -1;
-  hipLaunchKernelGGL(k_cfr_target_count, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap,
+  hipLaunchKernelGGL(k_cfr_target_count, dim3((B + CFR_WALK_TPW - 1) / CFR_WALK_TPW), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap,
                      edge_cap, roots, mode, counts);
   CHECK_LAUNCH();
 }
@@ -192,7 +205,7 @@ int cit_cfr_targets(void* pool, int B, int node_cap, int edge_cap, const int32_t
   if (B <= 0 || node_cap <= 0 || edge_cap <= 0 || !pool || !roots || !mt || !mt_idx || !offsets || mode < 0 ||
       mode > 3)
     return -1;
-  hipLaunchKernelGGL(k_cfr_targets, dim3((B + 63) / 64), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap, edge_cap,
+  hipLaunchKernelGGL(k_cfr_targets, dim3((B + CFR_WALK_TPW - 1) / CFR_WALK_TPW), dim3(64), 0, stream, (uint8_t*)pool, B, node_cap, edge_cap,
                      roots, mode, mt, mt_idx, offsets, meta, feat, value, dist, opt_feat);
   CHECK_LAUNCH();
 }

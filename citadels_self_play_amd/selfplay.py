@@ -111,6 +111,8 @@ ARENA_MIN_TREES, ARENA_MIN_BLOCKS = 32, 16
 # 1.25 61.4, 1.5 65.4 / 77.4, 2.0 61.0 (round 2's best), 2.5 63.2, 3.0 60.9
 # trees/s.
 QUEUE_OVERCOMMIT = float(os.environ.get("CIT_QUEUE_OVERCOMMIT", "1.5"))
+# share of the device memory not held by live tensors that node pools may take by default
+POOL_FRAC = float(os.environ.get("CIT_POOL_FRAC", "0.8"))
 # wall-clock seconds per queue slice (cit_cfr_train_slice's budget)
 QUEUE_SLICE_S = float(os.environ.get("CIT_QUEUE_SLICE_S", "0.5"))
 
@@ -150,7 +152,7 @@ def simulate_games(seeds, iters, max_move=100, node_cap=None, device=None, edge_
     dev = torch.device(device or "cuda")
     if max_pool_bytes is None:
         from .engine import device_avail_bytes   # (cached blocks of earlier pools count as free)
-        max_pool_bytes = int(0.8 * device_avail_bytes(dev))
+        max_pool_bytes = int(POOL_FRAC * device_avail_bytes(dev))
     seeds = np.asarray(seeds, np.int64)
     frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
     chunk = len(seeds)
@@ -337,7 +339,7 @@ class TreeQueue:
         self.t_setup = time.perf_counter()
         if max_pool_bytes is None:
             from .engine import device_avail_bytes
-            max_pool_bytes = int(0.8 * device_avail_bytes(dev))
+            max_pool_bytes = int(POOL_FRAC * device_avail_bytes(dev))
         frac = (lambda B: arena_frac_for(B, node_cap)) if arena_frac == "auto" else (lambda B: arena_frac)
         Q = max(1, int(per_round))
         if slots and multi_round:

@@ -316,9 +316,124 @@ CIT_HD int deck_take_like(CitGame& g, int c) {
 #ifndef CIT_SHUFFLE_REG
 #define CIT_SHUFFLE_REG 0
 #endif
+#ifndef CIT_SHUFFLE_BATCH
+#define CIT_SHUFFLE_BATCH 1
+#endif
+#if CIT_WAVE
+// The n - 1 draws of random.shuffle from a coop (LDS) stream, a chunk of up to
+// 64 stream words at a time instead of one _randbelow after another.  Draw t
+// (t = 0 .. n-2) is _randbelow(n - t): getrandbits(k) = word >> (32 - k),
+// rejected while >= n - t (Lib/random.py:239-249), so word q of a chunk is
+// tried by draw t0 + q - s, where s is the number of rejections before q.
+// Per chunk: lane q loads and tempers word q; one ballot per rejection finds
+// the next rejected word at the current s (every word before it is an
+// accepted draw); a ds_permute moves each accepted draw into lane t & 63 of
+// jv0 (t < 64) or jv1.  Same words, same order, same results as the serial
+// loop; the stream's position is advanced and its register window dropped.
+__device__ __forceinline__ void fy_draws_batched(CitMT& rng, int n, int& jv0, int& jv1) {
+  const int l = cit_lane();
+  uint32_t pos = rng.pos;
+  int t0 = 0;
+  while (t0 < n - 1) {
+    if (pos >= CIT_MT_N) {
+      if (CIT_TWIST_INLINE)
+        mt_twist_wave((cit_lds_u32*)rng.mt);
+      else
+        mt_twist_coop((cit_lds_u32*)rng.mt);
+      pos = 0;
+    }
+    const int L = CIT_MT_N - (int)pos < 64 ? CIT_MT_N - (int)pos : 64;   // words left before the twist
+    const int q = (int)pos + l;
+    const uint32_t word = mt_temper(((const cit_lds_u32*)rng.mt)[q < CIT_MT_N ? q : 0]);
+    uint64_t rej = 0;
+    int p = 0, s = 0, c;
+    const int n0 = n - t0 - l;   // lane l's bound at shift 0; at shift s it tries draw t0 + l - s, bound n0 + s
+    for (;;) {
+      const uint32_t N = (uint32_t)(n0 + s);
+      const uint64_t R0 = cit_ballot((word >> __builtin_clz(N | 1u)) >= N);   // (N | 1: clz(N) for N >= 2)
+      // the live lanes p .. hi: up to the last draw at this shift, or the chunk's end
+      const int e = n - 2 - t0 + s, hi = e < L - 1 ? e : L - 1;
+      const uint64_t R = R0 & (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & (~0ull << p);
+      if (!R) {   // every live word from p on is accepted
+        c = hi + 1;
+        break;
+      }
+      const int r = __ffsll((unsigned long long)R) - 1;
+      rej |= 1ull << r;
+      p = r + 1;
+      s++;
+      if (p >= L) {
+        c = L;
+        break;
+      }
+    }
+    const uint64_t acc = (c >= 64 ? ~0ull : ((1ull << c) - 1)) & ~rej;
+    const int nd = __popcll(acc);
+    const bool a = (acc >> l) & 1;
+    const int sl = __popcll(rej & cit_below());
+    const int t = t0 + l - sl;
+    const uint32_t N = (uint32_t)(n - t);
+    const int j = (int)(word >> __builtin_clz(N | 1u));
+    // accepted lane -> relative slot l - sl (its draw); the others fill the
+    // slots from nd on, in lane order: a permutation, no two lanes collide
+    const int slot = a ? l - sl : nd + __popcll(~acc & cit_below());
+    const int recv = __builtin_amdgcn_ds_permute(((t0 + slot) & 63) << 2, j);
+    const int k = (l - t0) & 63;   // this lane as a destination: draw t0 + k
+    if (k < nd) {
+      if (t0 + k < 64)
+        jv0 = recv;
+      else
+        jv1 = recv;
+    }
+    pos += (uint32_t)c;
+    t0 += nd;
+  }
+  rng.pos = pos;
+  rng.win_base = -1;
+}
+#endif
 template <class At>
 CIT_HD void shuffle_seq(CitMT& rng, int n, At at) {
 #if CIT_WAVE
+  if (CIT_SHUFFLE_BATCH && rng.coop && n > 1 && n <= 128) {
+    // all draws first (above), then each lane traces its element's final
+    // position back through the swaps (swap i is its own inverse, the last one
+    // first: a position p equal to i or to j moves to the other, p ^ (i ^ j)),
+    // one gather and one store of the sequence.  (Swaps of a one-VGPR sequence
+    // by readlane / writelane measured slower: ~117 against ~92 cycles per
+    // swap, tools/bench_shuffle.py.)
+    const int l = cit_lane();
+    int jv0 = 0, jv1 = 0;
+    fy_draws_batched(rng, n, jv0, jv1);
+    int p0 = l, p1 = l + 64;
+    if (n > 65) {
+      for (int t = n - 2; t >= 64; t--) {
+        const int i = n - 1 - t, j = __builtin_amdgcn_readlane(jv1, t - 64), x = i ^ j;
+        p0 = (p0 == i || p0 == j) ? p0 ^ x : p0;
+        p1 = (p1 == i || p1 == j) ? p1 ^ x : p1;
+      }
+    }
+    if (n > 64) {
+      for (int t = 63; t >= 0; t--) {
+        const int i = n - 1 - t, j = __builtin_amdgcn_readlane(jv0, t), x = i ^ j;
+        p0 = (p0 == i || p0 == j) ? p0 ^ x : p0;
+        p1 = (p1 == i || p1 == j) ? p1 ^ x : p1;
+      }
+    } else {
+#pragma unroll 4
+      for (int t = n - 2; t >= 0; t--) {
+        const int i = n - 1 - t, j = __builtin_amdgcn_readlane(jv0, t), x = i ^ j;
+        p0 = (p0 == i || p0 == j) ? p0 ^ x : p0;
+      }
+    }
+    const int x0 = l < n ? (int)at(l < n ? p0 : 0) : 0;
+    const int x1 = l + 64 < n ? (int)at(l + 64 < n ? p1 : 0) : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (l < n) at(l) = (uint8_t)x0;
+    if (l + 64 < n) at(l + 64) = (uint8_t)x1;
+    __builtin_amdgcn_wave_barrier();
+    return;
+  }
   if (CIT_SHUFFLE_REG && rng.coop && n > 1 && n <= 128) {
     // the sequence in two VGPRs (lane l: elements l and 64 + l); a swap is
     // two readlanes at wave-uniform indices and two lane selects, the same

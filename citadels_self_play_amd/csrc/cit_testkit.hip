@@ -122,6 +122,25 @@ __global__ __launch_bounds__(64) void k_bench_shuffle(int mode, int n, int reps,
         acc += v;
       }
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+    } else if (mode == 7 || mode == 8) {
+      // the batched draws alone (7), or followed by serial LDS swaps (8)
+      int jv0 = 0, jv1 = 0;
+      fy_draws_batched(r, n, jv0, jv1);
+      if (mode == 7) {
+        acc += (uint32_t)jv0 + (uint32_t)jv1;
+      } else {
+        for (int t = 0; t < n - 1; t++) {
+          const int i = n - 1 - t;
+          const int j = t < 64 ? __builtin_amdgcn_readlane(jv0, t) : __builtin_amdgcn_readlane(jv1, t - 64);
+          const uint8_t x = arr[i];
+          arr[i] = arr[j];
+          arr[j] = x;
+        }
+      }
+#endif
+    } else if (mode == 6) {
+      shuffle_arr(r, arr, n);   // the engine's coop path (CIT_SHUFFLE_BATCH: batched draws + traced swaps)
     } else if (mode == 1) {
       for (int i = n - 1; i > 0; i--) {
         const int j = (int)mt_randbelow(r, (uint32_t)(i + 1));
@@ -171,9 +190,72 @@ __global__ __launch_bounds__(64) void k_bench_shuffle(int mode, int n, int reps,
   }
 }
 
+// The batched shuffle (shuffle_seq under CIT_SHUFFLE_BATCH) against the
+// serial draws + swaps, from the same stream: block b copies words[b] (624
+// untempered MT words) into LDS, starts at pos0[b] and shuffles an identity
+// sequence of n `reps` times (crossing twists), recording each result
+// (out[batched][b][rep][n]) and, after the last, the stream position and
+// three further draws (tail[batched][b][4]).
+__global__ __launch_bounds__(64) void k_shuffle_check(int n, int reps, const uint32_t* words, const int* pos0,
+                                                     uint8_t* out, uint32_t* tail) {
+  __shared__ uint32_t mts[CIT_MT_N];
+  __shared__ uint8_t arr[128];
+  const int l = (int)threadIdx.x, b = (int)blockIdx.x, B = (int)gridDim.x;
+  for (int batched = 0; batched < 2; batched++) {
+    for (int i = l; i < CIT_MT_N; i += 64) mts[i] = words[(long)b * CIT_MT_N + i];
+    arr[l] = (uint8_t)l;
+    arr[l + 64] = (uint8_t)(l + 64);
+    __syncthreads();
+    CitMT r;
+    r.mt = mts;
+    r.stride = 1;
+    r.pos = (uint32_t)__builtin_amdgcn_readfirstlane(pos0[b]);
+    r.coop = CIT_MT_WINDOW;
+    r.win = 0;
+    r.win_base = -1;
+    const int nn = __builtin_amdgcn_readfirstlane(n);
+    for (int rep = 0; rep < reps; rep++) {
+      if (batched) {
+        shuffle_arr(r, arr, nn);
+      } else {
+        for (int i = nn - 1; i > 0; i--) {
+          const int j = (int)mt_randbelow(r, (uint32_t)(i + 1));
+          const uint8_t t = arr[i];
+          arr[i] = arr[j];
+          arr[j] = t;
+        }
+      }
+      __syncthreads();
+      uint8_t* o = out + (((long)batched * B + b) * reps + rep) * nn;
+      if (l < nn) o[l] = arr[l];
+      if (l + 64 < nn) o[l + 64] = arr[l + 64];
+      __syncthreads();
+    }
+    uint32_t* tl = tail + ((long)batched * B + b) * 4;
+    const uint32_t p = r.pos;
+    const uint32_t d0 = mt_randbelow(r, 1000u), d1 = mt_randbelow(r, 37u), d2 = mt_next(r);
+    if (l == 0) {
+      tl[0] = p;
+      tl[1] = d0;
+      tl[2] = d1;
+      tl[3] = d2;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// k_shuffle_check over `blocks` one-wave workgroups
+int citk_shuffle_check(int n, int reps, int blocks, const uint32_t* words, const int* pos0, uint8_t* out,
+                       uint32_t* tail, hipStream_t stream) {
+  if (n < 2 || n > 128 || reps < 1 || blocks < 1 || !words || !pos0 || !out || !tail) return -1;
+  hipLaunchKernelGGL(k_shuffle_check, dim3(blocks), dim3(64), 0, stream, n, reps, words, pos0, out, tail);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
 
 // k_bench_shuffle over `blocks` one-wave workgroups (out / sink: [blocks])
 int citk_bench_shuffle(int mode, int n, int reps, int blocks, unsigned long long* out, uint32_t* sink,

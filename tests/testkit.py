@@ -13,7 +13,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 _lib = None
 vp, i32 = C.c_void_p, C.c_int
 SIGS = {"citk_area_test": ([vp, vp, vp, i32, vp, i32, vp, vp], i32),
-        "citk_bench_shuffle": ([i32, i32, i32, i32, vp, vp, vp], i32)}
+        "citk_bench_shuffle": ([i32, i32, i32, i32, vp, vp, vp], i32),
+        "citk_shuffle_check": ([i32, i32, i32, vp, vp, vp, vp, vp], i32)}
 
 
 def sources():

@@ -13,7 +13,8 @@ import torch  # noqa: E402
 lib = testkit.lib()
 blocks = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 for n in (16, 60, 100):
-    for mode, name in enumerate(("draws_only", "lds_swaps", "reg_swaps", "traced", "draws_queue4", "draws_queue8")):
+    for mode, name in enumerate(("draws_only", "lds_swaps", "reg_swaps", "traced", "draws_queue4", "draws_queue8", "batched",
+                                  "batched_draws_only", "batched_draws_lds_swaps")):
         out = torch.zeros(blocks, dtype=torch.int64, device="cuda")
         sink = torch.zeros(blocks, dtype=torch.int32, device="cuda")
         for _ in range(2):

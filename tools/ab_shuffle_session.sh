@@ -16,9 +16,11 @@ for lib in build/abshuf/libcfrbase.so $M; do
   CIT_LIB_PATH=$lib timeout -k 10 120 python tools/bench_cfr.py --pred --batch 4096 --node-cap 4096 --reps 3 > $O/${v}_c4_$rep.log 2>&1 || exit 1
 done
 done
+if [ -z "$AB_QUICK" ]; then
 for rep in 1 2; do
 for lib in build/abshuf/librollbase.so $M; do
   timeout -k 10 150 python tools/_ablib.py $lib 4096 > $O/roll_$(basename $lib .so)_$rep.json 2> $O/roll_$(basename $lib .so)_$rep.err || exit 1
 done
 done
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests_cfr.txt 2>&1 || exit 1
+fi
+[ -n "$AB_QUICK" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests_cfr.txt 2>&1 || exit 1

@@ -319,6 +319,11 @@ CIT_HD int deck_take_like(CitGame& g, int c) {
 #ifndef CIT_SHUFFLE_BATCH
 #define CIT_SHUFFLE_BATCH 1
 #endif
+// below this length the serial draws are faster (tools/bench_shuffle.py: n = 3
+// 1.1 k vs 1.9 k cycles, n = 8 2.7 k vs 3.0 k, n = 12 even, n = 16 5.1 k vs 4.6 k)
+#ifndef CIT_SHUFFLE_BATCH_MIN
+#define CIT_SHUFFLE_BATCH_MIN 12
+#endif
 #if CIT_WAVE
 // The n - 1 draws of random.shuffle from a coop (LDS) stream, a chunk of up to
 // 64 stream words at a time instead of one _randbelow after another.  Draw t
@@ -395,7 +400,7 @@ __device__ __forceinline__ void fy_draws_batched(CitMT& rng, int n, int& jv0, in
 template <class At>
 CIT_HD void shuffle_seq(CitMT& rng, int n, At at) {
 #if CIT_WAVE
-  if (CIT_SHUFFLE_BATCH && rng.coop && n > 1 && n <= 128) {
+  if (CIT_SHUFFLE_BATCH && rng.coop && n >= CIT_SHUFFLE_BATCH_MIN && n > 1 && n <= 128) {
     // all draws first (above), then each lane traces its element's final
     // position back through the swaps (swap i is its own inverse, the last one
     // first: a position p equal to i or to j moves to the other, p ^ (i ^ j)),

@@ -2,7 +2,8 @@
 fy_draws_batched + traced swaps, CIT_SHUFFLE_BATCH) against the serial
 _randbelow draws and swaps (Lib/random.py:380-392, 239-249) from the same MT
 stream: the same sequences, the same stream position after, the same later
-draws.  Test-only kernel (tests/testkit.py)."""
+draws.  Test-only kernel (tests/testkit.py).  Lengths under
+CIT_SHUFFLE_BATCH_MIN (12) take the serial path in both runs."""
 import numpy as np
 import pytest
 

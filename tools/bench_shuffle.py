@@ -12,7 +12,8 @@ import torch  # noqa: E402
 
 lib = testkit.lib()
 blocks = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-for n in (16, 60, 100):
+NS = tuple(int(x) for x in sys.argv[2].split(",")) if len(sys.argv) > 2 else (16, 60, 100)
+for n in NS:
     for mode, name in enumerate(("draws_only", "lds_swaps", "reg_swaps", "traced", "draws_queue4", "draws_queue8", "batched",
                                   "batched_draws_only", "batched_draws_lds_swaps")):
         out = torch.zeros(blocks, dtype=torch.int64, device="cuda")
